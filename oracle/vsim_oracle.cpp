@@ -1,0 +1,671 @@
+// oracle/vsim_oracle.cpp — TEST INFRASTRUCTURE ONLY (parity checker, cpu_baseline).
+//
+// A CPU restatement of NAIST-Archlab/vsim's Q4_0 decode path, written from the
+// reference's behaviour (file:line cited per function).  Built with -O2 -msse3
+// -ffp-contract=off like the reference x86 build (Makefile-ubuntu:5-6): scalar code,
+// no FMA, ggml_float == double (ggml.c:66).  The product (libvsim_hip.so) never links
+// or calls this file; tests compare the HIP path against it, and it is itself pinned
+// bit-for-bit against the reference binary built from /root/reference (oracle/Makefile).
+
+#include "vsim_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr int QK = 32;
+constexpr int QBYTES = 20;  // sizeof(float) + QK/2, ggml.c:907-909
+
+// ---- fp16 <-> fp32 (bit-exact restatement of ggml.c:95-142) --------------------------
+inline float bits_f(uint32_t w) { float f; std::memcpy(&f, &w, 4); return f; }
+inline uint32_t f_bits(float f) { uint32_t w; std::memcpy(&w, &f, 4); return w; }
+
+float h2f(uint16_t h) {
+  const uint32_t w = (uint32_t)h << 16;
+  const uint32_t sign = w & 0x80000000u;
+  const uint32_t two_w = w + w;
+  const float normalized = bits_f((two_w >> 4) + (0xE0u << 23)) * 0x1.0p-112f;
+  const float denormalized = bits_f((two_w >> 17) | (126u << 23)) - 0.5f;
+  const uint32_t r = sign | (two_w < (1u << 27) ? f_bits(denormalized) : f_bits(normalized));
+  return bits_f(r);
+}
+
+uint16_t f2h(float f) {
+  float base = (std::fabs(f) * 0x1.0p+112f) * 0x1.0p-110f;
+  const uint32_t w = f_bits(f);
+  const uint32_t shl1_w = w + w;
+  const uint32_t sign = w & 0x80000000u;
+  uint32_t bias = shl1_w & 0xFF000000u;
+  if (bias < 0x71000000u) bias = 0x71000000u;
+  base = bits_f((bias >> 1) + 0x07800000u) + base;
+  const uint32_t bits = f_bits(base);
+  const uint32_t exp_bits = (bits >> 13) & 0x00007C00u;
+  const uint32_t mantissa_bits = bits & 0x00000FFFu;
+  const uint32_t nonsign = exp_bits + mantissa_bits;
+  return (uint16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+
+// ggml.c:1240-1251: the 64K tables built at first ggml_init
+float    g_f32_f16[65536];
+uint16_t g_gelu_f16[65536];
+uint16_t g_exp_f16[65536];
+bool     g_tables_ready = false;
+
+// ggml.c:789-791: GELU_COEF_A / SQRT_2_OVER_PI are ggml_float (double) constants
+float gelu_scalar(float x) {
+  const double A = 0.044715, S = 0.79788456;
+  return 0.5 * x * (1.0 + std::tanh(S * x * (1.0 + A * x * x)));
+}
+
+void init_tables_once() {
+  if (g_tables_ready) return;
+  for (int i = 0; i < 65536; ++i) {
+    const float f = g_f32_f16[i] = h2f((uint16_t)i);
+    g_gelu_f16[i] = f2h(gelu_scalar(f));
+    g_exp_f16[i] = f2h((float)std::exp((double)f));
+  }
+  g_tables_ready = true;
+}
+
+inline float lut_h2f(uint16_t h) { return g_f32_f16[h]; }
+
+// ---- Q4_0 -------------------------------------------------------------------------------
+// ggml.c:209-251 quantize_row_q4_0
+void quantize_row(const float *x, uint8_t *y, int k) {
+  const int nb = k / QK;
+  for (int i = 0; i < nb; i++) {
+    float amax = 0.0f;
+    for (int l = 0; l < QK; l++) {
+      const float v = x[i * QK + l];
+      amax = amax > std::fabs(v) ? amax : std::fabs(v);
+    }
+    const float d = amax / ((1 << 3) - 1);
+    const float id = d ? 1.0f / d : 0.0f;
+    std::memcpy(y + i * QBYTES, &d, 4);
+    uint8_t *pb = y + i * QBYTES + 4;
+    for (int l = 0; l < QK; l += 2) {
+      const float v0 = x[i * QK + l + 0] * id;
+      const float v1 = x[i * QK + l + 1] * id;
+      const uint8_t vi0 = (uint8_t)(((int8_t)std::round((double)v0)) + 8);
+      const uint8_t vi1 = (uint8_t)(((int8_t)std::round((double)v1)) + 8);
+      pb[l / 2] = (uint8_t)(vi0 | (vi1 << 4));
+    }
+  }
+}
+
+// ggml.c:301-334 dequantize_row_q4_0
+void dequantize_row(const uint8_t *x, float *y, int k) {
+  const int nb = k / QK;
+  for (int i = 0; i < nb; i++) {
+    float d;
+    std::memcpy(&d, x + i * QBYTES, 4);
+    const uint8_t *pp = x + i * QBYTES + 4;
+    for (int l = 0; l < QK; l += 2) {
+      const uint8_t vi = pp[l / 2];
+      const int8_t vi0 = vi & 0xf;
+      const int8_t vi1 = vi >> 4;
+      y[i * QK + l + 0] = (vi0 - 8) * d;
+      y[i * QK + l + 1] = (vi1 - 8) * d;
+    }
+  }
+}
+
+// imax.c:1191-1229 (== ggml_vec_dot_q4_0, ggml.c:472-511): one sequential float chain
+float vec_dot_q4(int n, const uint8_t *x, const uint8_t *y) {
+  const int nb = n / QK;
+  float sumf = 0.0f;
+  for (int i = 0; i < nb; i++) {
+    float d0, d1;
+    std::memcpy(&d0, x + i * QBYTES, 4);
+    std::memcpy(&d1, y + i * QBYTES, 4);
+    const uint8_t *p0 = x + i * QBYTES + 4;
+    const uint8_t *p1 = y + i * QBYTES + 4;
+    for (int j = 0; j < QK / 2; j++) {
+      const uint8_t v0 = p0[j];
+      const uint8_t v1 = p1[j];
+      const float f0 = d0 * ((int8_t)(v0 & 0xf) - 8);
+      const float f1 = d0 * ((int8_t)(v0 >> 4) - 8);
+      const float f2 = d1 * ((int8_t)(v1 & 0xf) - 8);
+      const float f3 = d1 * ((int8_t)(v1 >> 4) - 8);
+      sumf += f0 * f2 + f1 * f3;
+    }
+  }
+  return sumf;
+}
+
+template <class F>
+void parallel_rows(int nr, int nthreads, F &&fn) {
+  if (nthreads <= 1 || nr < 64) { fn(0, nr); return; }
+  std::vector<std::thread> th;
+  const int dr = (nr + nthreads - 1) / nthreads;  // ggml.c row split, imax.c:1184-1188
+  for (int t = 0; t < nthreads; ++t) {
+    const int r0 = dr * t, r1 = std::min(r0 + dr, nr);
+    if (r0 >= r1) break;
+    th.emplace_back([=, &fn] { fn(r0, r1); });
+  }
+  for (auto &t : th) t.join();
+}
+
+// ggml.c:4891-5165 + imax.c:1182-1230: dst[ic*M + ir] = dot(W row ir, xq row ic).
+// Rows are independent chains, so the result does not depend on nthreads.
+void mul_mat_q(const uint8_t *W, int M, int K, const uint8_t *xq, int N, float *y, int nthreads) {
+  const size_t rb = (size_t)K / QK * QBYTES;
+  parallel_rows(M, nthreads, [&](int r0, int r1) {
+    for (int ir = r0; ir < r1; ++ir)
+      for (int ic = 0; ic < N; ++ic) y[(size_t)ic * M + ir] = vec_dot_q4(K, W + ir * rb, xq + ic * rb);
+  });
+}
+
+void mul_mat_f(const uint8_t *W, int M, int K, const float *x, int N, float *y, int nthreads) {
+  const size_t rb = (size_t)K / QK * QBYTES;
+  std::vector<uint8_t> wdata(rb * N);  // INIT phase, ggml.c:5024-5041
+  for (int ic = 0; ic < N; ++ic) quantize_row(x + (size_t)ic * K, wdata.data() + ic * rb, K);
+  mul_mat_q(W, M, K, wdata.data(), N, y, nthreads);
+}
+
+// ggml.c:4246-4304 ggml_compute_forward_norm_f32
+void norm_row(const float *x, float *y, int n) {
+  const double eps = 1e-5f;
+  double mean = 0.0;
+  for (int i = 0; i < n; i++) mean += x[i];
+  mean /= n;
+  double sum2 = 0.0;
+  for (int i = 0; i < n; i++) {
+    double v = x[i] - mean;
+    y[i] = v;
+    sum2 += v * v;
+  }
+  const float scale = 1.0 / std::sqrt(sum2 / n + eps);
+  for (int i = 0; i < n; i++) y[i] *= scale;
+}
+
+// ggml.c:4113-4152 + 795-803: GELU through the fp16 table
+void gelu(const float *x, float *y, int n) {
+  for (int i = 0; i < n; i++) y[i] = lut_h2f(g_gelu_f16[f2h(x[i])]);
+}
+
+// ggml.c:5825-5893 ggml_compute_forward_soft_max_f32 (one row)
+void soft_max_row(float *p, int nc) {
+  double max = -INFINITY;
+  for (int i = 0; i < nc; ++i) max = max > p[i] ? max : p[i];
+  const float fmax_ = (float)max;
+  double sum = 0.0;
+  for (int i = 0; i < nc; i++) {
+    if (p[i] == -INFINITY) {
+      p[i] = 0.0f;
+    } else {
+      const uint16_t s = f2h(p[i] - fmax_);
+      const float val = lut_h2f(g_exp_f16[s]);
+      sum += val;
+      p[i] = val;
+    }
+  }
+  sum = 1.0 / sum;
+  const float v = (float)sum;
+  for (int i = 0; i < nc; i++) p[i] *= v;
+}
+
+// ggml.c:6086-6153 ggml_compute_forward_gptneox_rope_f32 (rotate-half)
+void rope_neox(float *x, int d, int H, int T, int n_past, int n_dims, int mode) {
+  for (int i2 = (mode == 0 ? 0 : n_past); i2 < T; i2++) {
+    const int p = (mode == 0 ? n_past + i2 : i2);
+    for (int i1 = 0; i1 < H; i1++) {
+      for (int i0 = 0; i0 < n_dims / 2; i0++) {
+        const double theta = std::pow(10000.0, 2 * ((double)-i0) / n_dims);
+        const double c = std::cos(p * theta), s = std::sin(p * theta);
+        float *v = x + ((size_t)i2 * H + i1) * d + i0;
+        const double x1 = v[0], x2 = v[n_dims / 2];
+        v[0] = (c * x1 - s * x2);
+        v[n_dims / 2] = (c * x2 + s * x1);
+      }
+    }
+  }
+}
+
+// ggml.c:5919-5974 ggml_compute_forward_rope_f32 (GPT-J interleaved pairs)
+void rope_gptj(float *x, int d, int H, int T, int n_past, int n_dims, int mode) {
+  for (int i2 = (mode == 0 ? 0 : n_past); i2 < T; i2++) {
+    const int p = (mode == 0 ? n_past + i2 : i2);
+    for (int i1 = 0; i1 < H; i1++) {
+      for (int i0 = 0; i0 < n_dims; i0 += 2) {
+        const double theta = std::pow(10000.0, ((double)-i0) / n_dims);
+        const double c = std::cos(p * theta), s = std::sin(p * theta);
+        float *v = x + ((size_t)i2 * H + i1) * d + i0;
+        const double x0 = v[0], x1 = v[1];
+        v[0] = x0 * c - x1 * s;
+        v[1] = x0 * s + x1 * c;
+      }
+    }
+  }
+}
+
+// ggml.c:4495-4534 (non-transposed src0) + ggml_vec_dot_f32 ggml.c:399-434
+void kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int N, float *out) {
+  for (int h = 0; h < H; ++h)
+    for (int k = 0; k < nk; ++k)
+      for (int q = 0; q < N; ++q) {
+        const float *kr = K + (size_t)k * ldk + h * d;
+        const float *qr = Q + (size_t)q * ldq + h * d;
+        double sumf = 0.0;
+        for (int i = 0; i < d; ++i) sumf += kr[i] * qr[i];
+        out[((size_t)h * N + q) * nk + k] = (float)sumf;
+      }
+}
+
+// ggml.c:4535-4581 (transposed src0, nth == 1) + ggml_vec_mad_f32 ggml.c:610-639
+void kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int N, float *out) {
+  for (int h = 0; h < H; ++h)
+    for (int q = 0; q < N; ++q) {
+      float *y = out + ((size_t)h * N + q) * d;
+      for (int i = 0; i < d; ++i) y[i] = 0.0f;
+      const float *srow = S + ((size_t)h * N + q) * nk;
+      for (int k = 0; k < nk; ++k) {
+        const float v = srow[k];
+        const float *x = V + (size_t)k * ldv + h * d;
+        for (int i = 0; i < d; ++i) y[i] += x[i] * v;
+      }
+    }
+}
+
+// ---- model --------------------------------------------------------------------------------
+struct Layer {
+  std::vector<float> ln1_w, ln1_b, ln2_w, ln2_b;
+  std::vector<uint8_t> wq, wk, wv, wo, wfc, wproj;
+  std::vector<float> bq, bk, bv, bo, bfc, bproj;
+};
+
+struct Model {
+  int arch = VO_ARCH_GPTNEOX;
+  int32_t n_vocab = 0, n_embd = 0, n_head = 0, n_layer = 0, n_rot = 0, par_res = 1, ftype = 2;
+  int n_ctx = 512;
+  std::vector<uint8_t> wte, lmh;
+  std::vector<float> lnf_w, lnf_b, lmh_b;
+  std::vector<Layer> layers;
+  std::vector<float> mem_k, mem_v;  // [L][n_ctx][E], vsim.cpp:349-366
+};
+
+bool read_all(std::ifstream &f, void *p, size_t n) {
+  f.read((char *)p, n);
+  return (size_t)f.gcount() == n;
+}
+
+// vsim.cpp:108-458 (GPT-NeoX) and convert_gptj_to_ggml.py:106-126 (GPT-J) formats.
+Model *load_model(const char *path, int arch, int n_ctx) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return nullptr;
+  uint32_t magic = 0;
+  read_all(f, &magic, 4);
+  if (magic != 0x67676d6c) return nullptr;
+  auto *m = new Model();
+  m->arch = arch;
+  m->n_ctx = n_ctx;
+  read_all(f, &m->n_vocab, 4);
+  read_all(f, &m->n_embd, 4);
+  read_all(f, &m->n_head, 4);
+  read_all(f, &m->n_layer, 4);
+  read_all(f, &m->n_rot, 4);
+  if (arch == VO_ARCH_GPTNEOX) read_all(f, &m->par_res, 4);
+  read_all(f, &m->ftype, 4);
+  int32_t nv = m->n_vocab;
+  if (arch == VO_ARCH_GPTJ) read_all(f, &nv, 4);  // explicit vocab count
+  for (int i = 0; i < nv; ++i) {
+    uint32_t len;
+    read_all(f, &len, 4);
+    std::string w(len, 0);
+    read_all(f, &w[0], len);
+  }
+  const int E = m->n_embd, L = m->n_layer, V = m->n_vocab;
+  m->layers.resize(L);
+  std::map<std::string, std::pair<void *, size_t>> slots;  // name -> (vector ptr, elem bytes kind)
+  auto f32slot = [&](const std::string &n, std::vector<float> &v, size_t ne) { v.resize(ne); slots[n] = {&v, 0}; };
+  auto q4slot = [&](const std::string &n, std::vector<uint8_t> &v, size_t ne) { v.resize(ne / QK * QBYTES); slots[n] = {&v, 1}; };
+  if (arch == VO_ARCH_GPTNEOX) {
+    q4slot("gpt_neox.embed_in.weight", m->wte, (size_t)E * V);
+    f32slot("gpt_neox.final_layer_norm.weight", m->lnf_w, E);
+    f32slot("gpt_neox.final_layer_norm.bias", m->lnf_b, E);
+    q4slot("embed_out.weight", m->lmh, (size_t)E * V);
+    for (int i = 0; i < L; ++i) {
+      auto &l = m->layers[i];
+      const std::string p = "gpt_neox.layers." + std::to_string(i) + ".";
+      f32slot(p + "input_layernorm.weight", l.ln1_w, E);
+      f32slot(p + "input_layernorm.bias", l.ln1_b, E);
+      f32slot(p + "post_attention_layernorm.weight", l.ln2_w, E);
+      f32slot(p + "post_attention_layernorm.bias", l.ln2_b, E);
+      q4slot(p + "attention.query.weight", l.wq, (size_t)E * E);
+      f32slot(p + "attention.query.bias", l.bq, E);
+      q4slot(p + "attention.key.weight", l.wk, (size_t)E * E);
+      f32slot(p + "attention.key.bias", l.bk, E);
+      q4slot(p + "attention.value.weight", l.wv, (size_t)E * E);
+      f32slot(p + "attention.value.bias", l.bv, E);
+      q4slot(p + "attention.dense.weight", l.wo, (size_t)E * E);
+      f32slot(p + "attention.dense.bias", l.bo, E);
+      q4slot(p + "mlp.dense_h_to_4h.weight", l.wfc, (size_t)E * 4 * E);
+      f32slot(p + "mlp.dense_h_to_4h.bias", l.bfc, 4 * E);
+      q4slot(p + "mlp.dense_4h_to_h.weight", l.wproj, (size_t)E * 4 * E);
+      f32slot(p + "mlp.dense_4h_to_h.bias", l.bproj, E);
+    }
+  } else {
+    q4slot("transformer.wte.weight", m->wte, (size_t)E * V);
+    f32slot("transformer.ln_f.weight", m->lnf_w, E);
+    f32slot("transformer.ln_f.bias", m->lnf_b, E);
+    q4slot("lm_head.weight", m->lmh, (size_t)E * V);
+    f32slot("lm_head.bias", m->lmh_b, V);
+    for (int i = 0; i < L; ++i) {
+      auto &l = m->layers[i];
+      const std::string p = "transformer.h." + std::to_string(i) + ".";
+      f32slot(p + "ln_1.weight", l.ln1_w, E);
+      f32slot(p + "ln_1.bias", l.ln1_b, E);
+      q4slot(p + "attn.q_proj.weight", l.wq, (size_t)E * E);
+      q4slot(p + "attn.k_proj.weight", l.wk, (size_t)E * E);
+      q4slot(p + "attn.v_proj.weight", l.wv, (size_t)E * E);
+      q4slot(p + "attn.out_proj.weight", l.wo, (size_t)E * E);
+      q4slot(p + "mlp.fc_in.weight", l.wfc, (size_t)E * 4 * E);
+      f32slot(p + "mlp.fc_in.bias", l.bfc, 4 * E);
+      q4slot(p + "mlp.fc_out.weight", l.wproj, (size_t)E * 4 * E);
+      f32slot(p + "mlp.fc_out.bias", l.bproj, E);
+    }
+  }
+  while (true) {
+    int32_t n_dims, length, ftype;
+    if (!read_all(f, &n_dims, 4)) break;
+    read_all(f, &length, 4);
+    read_all(f, &ftype, 4);
+    size_t ne = 1;
+    for (int i = 0; i < n_dims; ++i) {
+      int32_t d;
+      read_all(f, &d, 4);
+      ne *= d;
+    }
+    std::string name(length, 0);
+    read_all(f, &name[0], length);
+    auto it = slots.find(name);
+    if (it == slots.end()) {
+      fprintf(stderr, "oracle: unknown tensor '%s'\n", name.c_str());
+      delete m;
+      return nullptr;
+    }
+    if (it->second.second == 0) {
+      auto *v = (std::vector<float> *)it->second.first;
+      if (ftype != 0 || v->size() != ne) { delete m; return nullptr; }
+      read_all(f, v->data(), ne * 4);
+    } else {
+      auto *v = (std::vector<uint8_t> *)it->second.first;
+      if (ftype != 2 || v->size() != ne / QK * QBYTES) { delete m; return nullptr; }
+      read_all(f, v->data(), v->size());
+    }
+  }
+  m->mem_k.assign((size_t)L * n_ctx * E, 0.0f);
+  m->mem_v.assign((size_t)L * n_ctx * E, 0.0f);
+  return m;
+}
+
+void affine(std::vector<float> &x, const std::vector<float> &w, const std::vector<float> &b, int E, int N) {
+  // ggml_add(ggml_mul(ggml_repeat(w, x), x), ggml_repeat(b, x))
+  for (int t = 0; t < N; ++t)
+    for (int i = 0; i < E; ++i) x[(size_t)t * E + i] = (w[i] * x[(size_t)t * E + i]) + b[i];
+}
+
+void add_bias(std::vector<float> &x, const std::vector<float> &b, int E, int N) {
+  for (int t = 0; t < N; ++t)
+    for (int i = 0; i < E; ++i) x[(size_t)t * E + i] = x[(size_t)t * E + i] + b[i];
+}
+
+// vsim.cpp:470-747 (GPT-NeoX) ; the GPT-J graph is the same op sequence with ggml_rope
+// (ggml.c:5919-5974), one LayerNorm feeding attention and MLP, no q/k/v/out biases and a
+// biased lm_head.  Returns logits of the last token in `logits` (vsim.cpp:736-737).
+void eval(Model &m, int n_past, const int32_t *tok, int N, float *logits, int nthreads) {
+  const int E = m.n_embd, H = m.n_head, d = E / H, L = m.n_layer, V = m.n_vocab, F = 4 * E;
+  const int n_ctx = m.n_ctx;
+  const bool gptj = m.arch == VO_ARCH_GPTJ;
+  std::vector<float> inpL((size_t)E * N), cur((size_t)E * N), Q((size_t)E * N), Kc((size_t)E * N),
+      Vc((size_t)E * N), ff((size_t)E * N), fch((size_t)F * N), attn((size_t)E * N);
+  const size_t rbE = (size_t)E / QK * QBYTES;
+  for (int t = 0; t < N; ++t) dequantize_row(m.wte.data() + (size_t)tok[t] * rbE, inpL.data() + (size_t)t * E, E);
+  const int nk = n_past + N;
+  std::vector<float> KQ((size_t)H * N * nk), KQV((size_t)H * N * d);
+  // vsim.cpp:589: unqualified sqrt(float) binds ::sqrt(double) under -std=c++11
+  const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  for (int il = 0; il < L; ++il) {
+    Layer &l = m.layers[il];
+    for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
+    affine(cur, l.ln1_w, l.ln1_b, E, N);
+    mul_mat_f(l.wq.data(), E, E, cur.data(), N, Q.data(), nthreads);
+    mul_mat_f(l.wk.data(), E, E, cur.data(), N, Kc.data(), nthreads);
+    mul_mat_f(l.wv.data(), E, E, cur.data(), N, Vc.data(), nthreads);
+    if (!gptj) {
+      add_bias(Q, l.bq, E, N);
+      add_bias(Kc, l.bk, E, N);
+      add_bias(Vc, l.bv, E, N);
+    }
+    float *mk = m.mem_k.data() + (size_t)il * n_ctx * E;
+    float *mv = m.mem_v.data() + (size_t)il * n_ctx * E;
+    std::memcpy(mk + (size_t)n_past * E, Kc.data(), sizeof(float) * E * N);
+    std::memcpy(mv + (size_t)n_past * E, Vc.data(), sizeof(float) * E * N);
+    if (gptj) {
+      rope_gptj(Q.data(), d, H, N, n_past, m.n_rot, 0);
+      rope_gptj(mk, d, H, nk, n_past, m.n_rot, 1);
+    } else {
+      rope_neox(Q.data(), d, H, N, n_past, m.n_rot, 0);
+      rope_neox(mk, d, H, nk, n_past, m.n_rot, 1);
+    }
+    kq(mk, E, Q.data(), E, d, H, nk, N, KQ.data());
+    for (auto &v : KQ) v *= scale;
+    for (int h = 0; h < H; ++h)
+      for (int j = 0; j < N; ++j)
+        for (int i = n_past; i < nk; ++i)
+          if (i > n_past + j) KQ[((size_t)h * N + j) * nk + i] = -INFINITY;
+    for (int r = 0; r < H * N; ++r) soft_max_row(KQ.data() + (size_t)r * nk, nk);
+    kqv(mv, E, KQ.data(), d, H, nk, N, KQV.data());
+    for (int t = 0; t < N; ++t)
+      for (int h = 0; h < H; ++h)
+        for (int i = 0; i < d; ++i) cur[(size_t)t * E + h * d + i] = KQV[((size_t)h * N + t) * d + i];
+    mul_mat_f(l.wo.data(), E, E, cur.data(), N, attn.data(), nthreads);
+    if (!gptj) add_bias(attn, l.bo, E, N);  // bias + cur (commutative)
+    // feed-forward input: GPT-J reuses the ln_1 output; GPT-NeoX parallel residual
+    // normalises inpL again with post_attention_layernorm (vsim.cpp:660-696).
+    if (gptj) {
+      for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, ff.data() + (size_t)t * E, E);
+      affine(ff, l.ln1_w, l.ln1_b, E, N);
+    } else if (m.par_res == 1) {
+      for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, ff.data() + (size_t)t * E, E);
+      affine(ff, l.ln2_w, l.ln2_b, E, N);
+    } else {
+      for (size_t i = 0; i < ff.size(); ++i) ff[i] = attn[i] + inpL[i];
+      std::vector<float> tmp(ff.size());
+      for (int t = 0; t < N; ++t) norm_row(ff.data() + (size_t)t * E, tmp.data() + (size_t)t * E, E);
+      ff.swap(tmp);
+      affine(ff, l.ln2_w, l.ln2_b, E, N);
+    }
+    mul_mat_f(l.wfc.data(), F, E, ff.data(), N, fch.data(), nthreads);
+    add_bias(fch, l.bfc, F, N);
+    gelu(fch.data(), fch.data(), F * N);
+    mul_mat_f(l.wproj.data(), E, F, fch.data(), N, ff.data(), nthreads);
+    add_bias(ff, l.bproj, E, N);
+    if (gptj || m.par_res == 1) {
+      for (size_t i = 0; i < inpL.size(); ++i) inpL[i] = inpL[i] + (attn[i] + ff[i]);
+    } else {
+      for (size_t i = 0; i < inpL.size(); ++i) inpL[i] = ff[i] + (attn[i] + inpL[i]);
+    }
+  }
+  for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
+  affine(cur, m.lnf_w, m.lnf_b, E, N);
+  // lm_head over all N rows (vsim.cpp:716-718); only the last row is returned
+  std::vector<float> lg((size_t)V * N);
+  mul_mat_f(m.lmh.data(), V, E, cur.data(), N, lg.data(), nthreads);
+  if (gptj) add_bias(lg, m.lmh_b, V, N);
+  std::memcpy(logits, lg.data() + (size_t)V * (N - 1), sizeof(float) * V);
+}
+
+// utils.cpp:339-422 sample_top_p_top_k_repeat_penalty
+int sample(const float *logits, int n_logits, std::vector<int32_t> &last_n, double repeat_penalty, int top_k,
+           double top_p, double temp, std::mt19937 &rng) {
+  std::vector<std::pair<double, int32_t>> logits_id;
+  logits_id.reserve(n_logits);
+  const double scale = 1.0 / temp;
+  for (int i = 0; i < n_logits; ++i) {
+    if (std::find(last_n.begin(), last_n.end(), i) != last_n.end()) {
+      if (logits[i] < 0.0)
+        logits_id.push_back(std::make_pair(logits[i] * scale * repeat_penalty, i));
+      else
+        logits_id.push_back(std::make_pair(logits[i] * scale / repeat_penalty, i));
+    } else {
+      logits_id.push_back(std::make_pair(logits[i] * scale, i));
+    }
+  }
+  std::partial_sort(logits_id.begin(), logits_id.begin() + top_k, logits_id.end(),
+                    [](const std::pair<double, int32_t> &a, const std::pair<double, int32_t> &b) {
+                      return a.first > b.first;
+                    });
+  logits_id.resize(top_k);
+  double maxl = -INFINITY;
+  for (const auto &kv : logits_id) maxl = std::max(maxl, kv.first);
+  std::vector<double> probs;
+  probs.reserve(logits_id.size());
+  double sum = 0.0;
+  for (const auto &kv : logits_id) {
+    double p = std::exp(kv.first - maxl);
+    probs.push_back(p);
+    sum += p;
+  }
+  for (auto &p : probs) p /= sum;
+  if (top_p < 1.0f) {
+    double cumsum = 0.0f;
+    for (int i = 0; i < (int)probs.size(); i++) {
+      cumsum += probs[i];
+      if (cumsum >= top_p) {
+        probs.resize(i + 1);
+        logits_id.resize(i + 1);
+        break;
+      }
+    }
+    cumsum = 1.0 / cumsum;
+    for (int i = 0; i < (int)probs.size(); i++) probs[i] *= cumsum;
+  }
+  std::discrete_distribution<> dist(probs.begin(), probs.end());
+  int idx = dist(rng);
+  return logits_id[idx].second;
+}
+
+}  // namespace
+
+extern "C" {
+
+void vo_init_tables(void) { init_tables_once(); }
+float vo_fp16_to_fp32(uint16_t h) { return h2f(h); }
+uint16_t vo_fp32_to_fp16(float f) { return f2h(f); }
+void vo_tables(uint16_t *exp_f16, uint16_t *gelu_f16) {
+  init_tables_once();
+  std::memcpy(exp_f16, g_exp_f16, sizeof(g_exp_f16));
+  std::memcpy(gelu_f16, g_gelu_f16, sizeof(g_gelu_f16));
+}
+
+void vo_quantize_row_q4_0(const float *x, void *y, int k) { quantize_row(x, (uint8_t *)y, k); }
+void vo_dequantize_row_q4_0(const void *x, float *y, int k) { dequantize_row((const uint8_t *)x, y, k); }
+void vo_vec_dot_q4_0(int n, float *s, const void *x, const void *y) {
+  *s = vec_dot_q4(n, (const uint8_t *)x, (const uint8_t *)y);
+}
+void vo_mul_mat_q4_0_f32(const void *W, int M, int K, const float *x, int N, float *y, int nthreads) {
+  mul_mat_f((const uint8_t *)W, M, K, x, N, y, nthreads);
+}
+void vo_mul_mat_q4_0_q(const void *W, int M, int K, const void *xq, int N, float *y, int nthreads) {
+  mul_mat_q((const uint8_t *)W, M, K, (const uint8_t *)xq, N, y, nthreads);
+}
+void vo_norm_f32(const float *x, float *y, int n, int rows) {
+  for (int r = 0; r < rows; ++r) norm_row(x + (size_t)r * n, y + (size_t)r * n, n);
+}
+void vo_gelu_f32(const float *x, float *y, int n) { init_tables_once(); gelu(x, y, n); }
+void vo_soft_max_f32(float *p, int nc, int nr) {
+  init_tables_once();
+  for (int r = 0; r < nr; ++r) soft_max_row(p + (size_t)r * nc, nc);
+}
+void vo_scale_f32(float *p, int n, float v) { for (int i = 0; i < n; ++i) p[i] *= v; }
+void vo_diag_mask_inf_f32(float *p, int nc, int nr, int nz, int n_past) {
+  for (int k = 0; k < nz; k++)
+    for (int j = 0; j < nr; j++)
+      for (int i = n_past; i < nc; i++)
+        if (i > n_past + j) p[((size_t)k * nr + j) * nc + i] = -INFINITY;
+}
+void vo_rope_neox(float *x, int d, int H, int T, int n_past, int n_dims, int mode) {
+  rope_neox(x, d, H, T, n_past, n_dims, mode);
+}
+void vo_rope_gptj(float *x, int d, int H, int T, int n_past, int n_dims, int mode) {
+  rope_gptj(x, d, H, T, n_past, n_dims, mode);
+}
+void vo_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int N, float *KQ) {
+  kq(K, ldk, Q, ldq, d, H, nk, N, KQ);
+}
+void vo_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int N, float *out) {
+  kqv(V, ldv, S, d, H, nk, N, out);
+}
+void vo_get_rows_q4_0(const void *W, int K, const int32_t *rows, int n, float *y) {
+  const size_t rb = (size_t)K / QK * QBYTES;
+  for (int i = 0; i < n; ++i) dequantize_row((const uint8_t *)W + rows[i] * rb, y + (size_t)i * K, K);
+}
+
+void *vo_model_load(const char *path, int arch, int n_ctx) {
+  init_tables_once();
+  return load_model(path, arch, n_ctx);
+}
+void vo_model_hparams(void *mp, int32_t *o) {
+  auto *m = (Model *)mp;
+  o[0] = m->n_vocab; o[1] = m->n_embd; o[2] = m->n_head; o[3] = m->n_layer;
+  o[4] = m->n_rot; o[5] = m->par_res; o[6] = m->ftype; o[7] = m->n_ctx;
+}
+int vo_model_eval(void *mp, int n_past, const int32_t *tokens, int N, float *logits, int nthreads) {
+  auto *m = (Model *)mp;
+  if (N <= 0 || n_past + N > m->n_ctx) return -1;
+  eval(*m, n_past, tokens, N, logits, nthreads);
+  return 0;
+}
+void vo_model_free(void *mp) { delete (Model *)mp; }
+
+// vsim.cpp:749-910 main_gptneox decode loop; returns the ids it prints between
+// "<|BEGIN>" and "<END|>" (prompt echoed in n_batch+1 chunks, then sampled ids).
+int vo_generate(void *mp, const int32_t *prompt, int n_prompt, int n_predict, int seed, int top_k, float top_p,
+                float temp, int repeat_last_n, float repeat_penalty, int n_batch, int32_t *out, int out_cap,
+                int nthreads) {
+  auto *m = (Model *)mp;
+  std::mt19937 rng(seed);
+  std::vector<int32_t> embd_inp(prompt, prompt + n_prompt);
+  n_predict = std::min(n_predict, m->n_ctx - (int)embd_inp.size());
+  std::vector<float> logits(m->n_vocab);
+  const int32_t warm[5] = {1, 2, 3, 4, 5};
+  eval(*m, 0, warm, 5, logits.data(), nthreads);
+  std::vector<int32_t> last_n(repeat_last_n, 0);
+  std::vector<int32_t> embd;
+  int n_past = 0, n_out = 0;
+  for (int i = (int)embd.size(); i < (int)embd_inp.size() + n_predict; i++) {
+    if (!embd.empty()) eval(*m, n_past, embd.data(), (int)embd.size(), logits.data(), nthreads);
+    n_past += (int)embd.size();
+    embd.clear();
+    if (i >= (int)embd_inp.size()) {
+      const int id = sample(logits.data(), m->n_vocab, last_n, repeat_penalty, (int)(float)top_k, top_p, temp, rng);
+      last_n.erase(last_n.begin());
+      last_n.push_back(id);
+      embd.push_back(id);
+    } else {
+      for (int k = i; k < (int)embd_inp.size(); k++) {
+        embd.push_back(embd_inp[k]);
+        last_n.erase(last_n.begin());
+        last_n.push_back(embd_inp[k]);
+        if ((int)embd.size() > n_batch) break;
+      }
+      i += (int)embd.size() - 1;
+    }
+    for (auto id : embd)
+      if (n_out < out_cap) out[n_out++] = id;
+    if (embd.back() == 2) break;
+  }
+  return n_out;
+}
+
+}  // extern "C"
