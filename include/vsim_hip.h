@@ -1,0 +1,149 @@
+/* include/vsim_hip.h — C-ABI of libvsim_hip.so, the MI355X (gfx950) replacement for the
+ * reference's imax.c / emax7lib.c offload layer.
+ *
+ * Three layers, all plain C types (no torch / HIP types in any signature):
+ *
+ *  1. Drop-in entry points with the reference's own symbol names and signatures, so a
+ *     reference build links libvsim_hip.so where it linked imax.o:
+ *       init_xmax()                                   replaces imax.c:52-142
+ *       imax_ggml_compute_forward_mul_mat_q4_0_f32()  replaces imax.c:1133-2292
+ *                                                     (called from ggml.c:5115)
+ *     plus vsim_ggml_* hooks for the ops that have no offload boundary in the reference
+ *     (RoPE ggml.c:6086/5919, soft_max ggml.c:5825, KQ/KQV mul_mat ggml.c:4355).
+ *  2. Op-level device API (vsim_op_*): every hot op on device pointers, in the exact
+ *     (reference-bit-identical) or fast numeric mode.  Used by the parity tests.
+ *  3. Model-level executor (vsim_model_*): device-resident GPT-NeoX (vsim.cpp:470-747)
+ *     and GPT-J graphs, whole decode step captured in a hipGraph; host<->device traffic
+ *     per token is the token ids in and one logits row out (vsim.cpp:736-737).
+ *
+ * Device weight layout ("Q4 SoA"): a Q4_0 matrix of M rows x K weights keeps the
+ * reference's 0.625 B/weight but splits the 20-byte blocks (ggml.c:204-251) into a
+ * 16-byte-aligned nibble plane qs[M][K/32][16] followed by the scale plane d[M][K/32]
+ * (fp32).  vsim_q4_bytes(M, K) == M*K/32*20 bytes.
+ *
+ * Every function returns 0 on success or a negative VSIM_E* code; vsim_last_error()
+ * describes the last failure of the calling thread.
+ */
+#ifndef VSIM_HIP_H
+#define VSIM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ggml_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSIM_OK 0
+#define VSIM_EINVAL (-1)
+#define VSIM_EHIP (-2)
+#define VSIM_ENOMEM (-3)
+#define VSIM_EFILE (-4)
+#define VSIM_ENODEV (-5)
+
+/* numeric modes */
+#define VSIM_MODE_EXACT 0 /* bit-identical to the reference at --threads 1            */
+#define VSIM_MODE_FAST 1  /* split-K integer-dot GEMV: same math, different rounding  */
+
+/* architectures */
+#define VSIM_ARCH_GPTNEOX 0 /* vsim.cpp:470-747                                      */
+#define VSIM_ARCH_GPTJ 1    /* ggml GPT-J graph composed from the same ops           */
+
+const char *vsim_last_error(void);
+int vsim_device_count(void);
+size_t vsim_q4_bytes(int rows, int k);
+
+/* ---------------------------------------------------------------- 1. drop-in ----- */
+void init_xmax(void);
+void imax_ggml_compute_forward_mul_mat_q4_0_f32(int THREAD, int LANE, const struct ggml_compute_params *params,
+                                                const struct ggml_tensor *src0, const struct ggml_tensor *src1,
+                                                struct ggml_tensor *dst);
+/* New hooks (same (params, src0, src1, dst) shape as the static ggml.c kernels they
+ * replace; host tensors in, host tensors out, exact mode).  Return 0 if handled. */
+int vsim_ggml_gptneox_rope_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
+                               const struct ggml_tensor *src1, struct ggml_tensor *dst);
+int vsim_ggml_rope_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
+                       const struct ggml_tensor *src1, struct ggml_tensor *dst);
+int vsim_ggml_soft_max_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
+                           struct ggml_tensor *dst);
+int vsim_ggml_mul_mat_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
+                          const struct ggml_tensor *src1, struct ggml_tensor *dst);
+/* drop-in statistics: calls, bytes moved host<->device, device weight-cache size */
+void vsim_dropin_stats(uint64_t *calls, uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *cached_bytes);
+void vsim_dropin_reset(void);
+
+/* ------------------------------------------------------- 2. op-level (device ptrs) -- */
+/* `stream` is a hipStream_t passed as void* (NULL = default stream). */
+int vsim_op_q4_repack(const void *aos, void *soa, int rows, int k, void *stream);
+int vsim_op_q4_unpack(const void *soa, void *aos, int rows, int k, void *stream);
+/* quantize_row_q4_0 (ggml.c:209-251) of n rows of k floats: xq in Q4 SoA, xd = the
+ * dequantized values d*(q-8) the exact GEMV multiplies with (ggml.c:497-498). */
+int vsim_op_q4_quantize(const float *x, int k, int n, void *xq, float *xd, void *stream);
+/* y[n][M] = W[M][K] . q4_0(x)[n][K] (+ bias[M] if bias != NULL, added after the dot
+ * as ggml_add does, vsim.cpp:545-547) */
+int vsim_op_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias,
+                    float *y, int mode, void *stream);
+int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream);
+/* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
+int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);
+int vsim_op_gelu(const float *x, float *y, int n, void *stream);
+/* scale -> diag_mask_inf(n_past) -> soft_max over p[nz][nr][nc], in place */
+int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream);
+/* style 0 = GPT-NeoX rotate-half (ggml.c:6086), 1 = GPT-J pairs (ggml.c:5919);
+ * x[T][H][d] in place; mode 0: p = n_past+i2, mode 1: i2 >= n_past only, p = i2 */
+int vsim_op_rope(int style, float *x, int d, int H, int T, int n_past, int n_dims, int mode, void *stream);
+int vsim_op_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq,
+               void *stream);
+int vsim_op_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, void *stream);
+/* device fp16 tables (exp, gelu) as built by ggml_init (ggml.c:1240-1251) */
+int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host);
+
+/* ------------------------------------------------------ 3. model-level executor ---- */
+typedef struct vsim_model vsim_model;
+
+typedef struct {
+  int32_t n_vocab, n_embd, n_head, n_layer, n_rot, use_parallel_residual;
+} vsim_hparams;
+
+/* Layers [layer_begin, layer_end) live on `device`; the first stage also owns the
+ * embedding, the last stage ln_f + lm_head. */
+int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
+                      vsim_model **out);
+/* Load a ggml model file of `arch` (vsim.cpp:108-458 / convert_gptj_to_ggml.py format);
+ * creates the model, uploads every tensor this stage owns. */
+int vsim_model_load_file(const char *path, int arch, int n_ctx, int device, int layer_begin, int layer_end,
+                         vsim_model **out);
+/* Upload one tensor by its ggml-file name (Q4_0 tensors in the on-disk AoS format). */
+int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes);
+/* Synthetic weights drawn on the device (N(0,std), LN gains 1+N(0,std)), quantized with
+ * quantize_row_q4_0 semantics; for throughput runs of full-size configs. */
+int vsim_model_randomize(vsim_model *m, uint64_t seed, float std);
+int vsim_model_set_mode(vsim_model *m, int mode);
+int vsim_model_hparams(const vsim_model *m, vsim_hparams *hp, int *n_ctx, int *layer_begin, int *layer_end);
+/* One eval of N tokens at n_past (vsim.cpp:470-747).  First stage reads `tokens`;
+ * non-first stages read the residual from `resid_in` (device, [N][n_embd] f32);
+ * non-last stages write their residual to `resid_out` (device); the last stage copies
+ * the last row of logits to `logits` (host, n_vocab floats) if non-NULL. */
+int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, const float *resid_in,
+                    float *resid_out, float *logits);
+/* Decode-step timing helpers for bench.py: the stream the executor launches on, and
+ * device pointers of the last logits / residual buffers. */
+void *vsim_model_stream(vsim_model *m);
+const float *vsim_model_logits_dev(vsim_model *m);
+/* Number of kernels one eval launches; whether the decode step replays a hipGraph. */
+int vsim_model_info(vsim_model *m, int *kernels_per_eval, int *graph_enabled, size_t *weight_bytes);
+int vsim_model_set_graph(vsim_model *m, int enable);
+/* GEMV profiling for the live roofline: when enabled, an event pair brackets every Q4_0
+ * GEMV launch on the model's stream; stats accumulate the summed GEMV device time, the
+ * launch count and the algorithmic weight bytes those launches read. */
+int vsim_model_set_profile(vsim_model *m, int enable);
+int vsim_model_profile_stats(vsim_model *m, double *gemv_ms, long *gemv_launches, double *gemv_bytes);
+void vsim_model_free(vsim_model *m);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSIM_HIP_H */

@@ -493,7 +493,8 @@ void eval(Model &m, int n_past, const int32_t *tok, int N, float *logits, int nt
     if (gptj || m.par_res == 1) {
       for (size_t i = 0; i < inpL.size(); ++i) inpL[i] = inpL[i] + (attn[i] + ff[i]);
     } else {
-      for (size_t i = 0; i < inpL.size(); ++i) inpL[i] = ff[i] + (attn[i] + inpL[i]);
+      // vsim.cpp:657: inpL = ggml_add(inpFF, inpL) — only the FF output is added back
+      for (size_t i = 0; i < inpL.size(); ++i) inpL[i] = ff[i] + inpL[i];
     }
   }
   for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
@@ -615,6 +616,64 @@ void *vo_model_load(const char *path, int arch, int n_ctx) {
   init_tables_once();
   return load_model(path, arch, n_ctx);
 }
+// Synthetic weights generated in place (cpu_baseline sample of a full-width config):
+// N(0, std) matrices / biases, 1 + N(0, std) LN gains, quantized with quantize_row_q4_0.
+void *vo_model_synthetic(int arch, int n_vocab, int n_embd, int n_head, int n_layer, int n_rot, int n_ctx,
+                         uint64_t seed, float stddev) {
+  init_tables_once();
+  auto *m = new Model();
+  m->arch = arch;
+  m->n_vocab = n_vocab; m->n_embd = n_embd; m->n_head = n_head; m->n_layer = n_layer; m->n_rot = n_rot;
+  m->par_res = 1; m->ftype = 2; m->n_ctx = n_ctx;
+  const int E = n_embd, F = 4 * E, V = n_vocab;
+  // counter-seeded xorshift64* per row so rows can be generated in parallel
+  auto rowgen = [](uint64_t st, float *out, int k, float sd) {
+    st = st * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+    for (int i = 0; i < k; i += 2) {
+      st ^= st >> 12; st ^= st << 25; st ^= st >> 27;
+      const uint64_t a = st * 0x2545F4914F6CDD1Dull;
+      st ^= st >> 12; st ^= st << 25; st ^= st >> 27;
+      const uint64_t b = st * 0x2545F4914F6CDD1Dull;
+      const float u1 = ((a >> 40) + 1) * (1.0f / 16777217.0f), u2 = (b >> 40) * (1.0f / 16777216.0f);
+      const float r = std::sqrt(-2.0f * std::log(u1)) * sd;
+      out[i] = r * std::cos(6.2831853f * u2);
+      if (i + 1 < k) out[i + 1] = r * std::sin(6.2831853f * u2);
+    }
+  };
+  uint64_t tensor_id = seed << 20;
+  const int nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  auto q4 = [&](std::vector<uint8_t> &v, size_t rows, int k) {
+    v.resize(rows * (k / QK) * QBYTES);
+    const uint64_t tid = ++tensor_id;
+    parallel_rows((int)rows, nth, [&](int r0, int r1) {
+      std::vector<float> tmp(k);
+      for (int r = r0; r < r1; ++r) {
+        rowgen((tid << 32) ^ (uint64_t)r, tmp.data(), k, stddev);
+        quantize_row(tmp.data(), v.data() + (size_t)r * (k / QK) * QBYTES, k);
+      }
+    });
+  };
+  auto f32 = [&](std::vector<float> &v, int n, float mean) {
+    v.resize(n);
+    rowgen(++tensor_id, v.data(), n, stddev);
+    for (auto &x : v) x += mean;
+  };
+  q4(m->wte, V, E);
+  q4(m->lmh, V, E);
+  f32(m->lnf_w, E, 1.0f); f32(m->lnf_b, E, 0.0f); f32(m->lmh_b, V, 0.0f);
+  m->layers.resize(n_layer);
+  for (auto &l : m->layers) {
+    f32(l.ln1_w, E, 1.0f); f32(l.ln1_b, E, 0.0f); f32(l.ln2_w, E, 1.0f); f32(l.ln2_b, E, 0.0f);
+    q4(l.wq, E, E); q4(l.wk, E, E); q4(l.wv, E, E); q4(l.wo, E, E);
+    q4(l.wfc, F, E); q4(l.wproj, E, F);
+    f32(l.bq, E, 0.0f); f32(l.bk, E, 0.0f); f32(l.bv, E, 0.0f); f32(l.bo, E, 0.0f);
+    f32(l.bfc, F, 0.0f); f32(l.bproj, E, 0.0f);
+  }
+  m->mem_k.assign((size_t)n_layer * n_ctx * E, 0.0f);
+  m->mem_v.assign((size_t)n_layer * n_ctx * E, 0.0f);
+  return m;
+}
+
 void vo_model_hparams(void *mp, int32_t *o) {
   auto *m = (Model *)mp;
   o[0] = m->n_vocab; o[1] = m->n_embd; o[2] = m->n_head; o[3] = m->n_layer;

@@ -26,6 +26,8 @@ def lib():
         L.vo_model_load.restype = vp
         L.vo_model_load.argtypes = [ctypes.c_char_p, ci, ci]
         L.vo_model_eval.argtypes = [vp, ci, vp, ci, vp, ci]
+        L.vo_model_synthetic.restype = vp
+        L.vo_model_synthetic.argtypes = [ci, ci, ci, ci, ci, ci, ci, ctypes.c_uint64, cf]
         L.vo_model_hparams.argtypes = [vp, vp]
         L.vo_model_free.argtypes = [vp]
         L.vo_generate.argtypes = [vp, vp, ci, ci, ci, ci, cf, cf, ci, cf, ci, vp, ci, ci]
@@ -130,8 +132,12 @@ def tables():
 
 
 class Model:
-    def __init__(self, path: str, arch: int, n_ctx: int = 512):
-        self.h = lib().vo_model_load(path.encode(), arch, n_ctx)
+    def __init__(self, path, arch: int, n_ctx: int = 512, synthetic=None):
+        if synthetic is not None:  # (n_vocab, n_embd, n_head, n_layer, n_rot, seed, std)
+            nv, ne, nh, nl, nr, seed, std = synthetic
+            self.h = lib().vo_model_synthetic(arch, nv, ne, nh, nl, nr, n_ctx, seed, std)
+        else:
+            self.h = lib().vo_model_load(path.encode(), arch, n_ctx)
         if not self.h:
             raise RuntimeError(f"oracle could not load {path}")
         hp = np.zeros(8, np.int32)

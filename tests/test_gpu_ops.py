@@ -1,0 +1,209 @@
+"""Per-op parity of the HIP kernels (through the C-ABI) against the reference's own
+outputs (tests/golden/ops_*.npz, produced by the reference ggml ops at --threads 1).
+
+Exact mode must be bit-identical.  The fast GEMV is checked against an fp64 evaluation
+of the same Q4_0 x Q4_0 product with an error bound (tolerance written below).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from golden_util import cases, ops  # noqa: E402
+from vsim_amd import hip  # noqa: E402
+from vsim_amd import modelgen as mg  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def repack(aos_np, rows, k):
+    src = dev(aos_np)
+    dst = torch.empty(hip.q4_bytes(rows, k), dtype=torch.uint8, device=DEV)
+    hip.check(hip.lib().vsim_op_q4_repack(src.data_ptr(), dst.data_ptr(), rows, k, None), "repack")
+    return dst
+
+
+def quantize(x_np, k, n):
+    x = dev(x_np.astype(np.float32))
+    xq = torch.empty(hip.q4_bytes(n, k), dtype=torch.uint8, device=DEV)
+    xd = torch.empty(n * k, dtype=torch.float32, device=DEV)
+    hip.check(hip.lib().vsim_op_q4_quantize(x.data_ptr(), k, n, xq.data_ptr(), xd.data_ptr(), None), "quantize")
+    return xq, xd
+
+
+def gemv(w, M, K, xq, xd, n, mode, bias=None):
+    y = torch.empty(n * M, dtype=torch.float32, device=DEV)
+    hip.check(hip.lib().vsim_op_q4_gemv(w.data_ptr(), M, K, xq.data_ptr(), xd.data_ptr(), n,
+                                        None if bias is None else bias.data_ptr(), y.data_ptr(), mode, None), "gemv")
+    return host(y)
+
+
+def test_repack_roundtrip():
+    rng = np.random.default_rng(0)
+    aos = mg.quantize_q4_0(rng.standard_normal(96 * 256).astype(np.float32))
+    soa = repack(aos, 96, 256)
+    back = torch.empty_like(soa)
+    hip.check(hip.lib().vsim_op_q4_unpack(soa.data_ptr(), back.data_ptr(), 96, 256, None), "unpack")
+    assert np.array_equal(host(back), aos)
+
+
+def test_quantize_bit_exact():
+    z = ops("qrow")
+    x = z["x"]
+    xq, _ = quantize(x, x.size, 1)
+    aos = torch.empty_like(xq)
+    hip.check(hip.lib().vsim_op_q4_unpack(xq.data_ptr(), aos.data_ptr(), 1, x.size, None), "unpack")
+    assert np.array_equal(host(aos), z["y"])
+
+
+@pytest.mark.parametrize("c", cases(ops("mulmat")), ids=lambda c: "x".join(map(str, c["shape"])))
+def test_gemv_exact_bit_exact(c):
+    M, K, N = (int(v) for v in c["shape"])
+    w = repack(c["w"], M, K)
+    xq, xd = quantize(c["x"], K, N)
+    y = gemv(w, M, K, xq, xd, N, hip.MODE_EXACT)
+    assert np.array_equal(bits(y), bits(c["y"]))
+
+
+def _fp64_product(w_aos, M, K, xq_aos, N):
+    W = mg.dequantize_q4_0(w_aos, K).astype(np.float64)       # [M, K]
+    X = mg.dequantize_q4_0(xq_aos, K).astype(np.float64)      # [N, K]
+    return (X @ W.T), (np.abs(X) @ np.abs(W).T)
+
+
+@pytest.mark.parametrize("c", cases(ops("mulmat")), ids=lambda c: "x".join(map(str, c["shape"])))
+def test_gemv_fast_within_bound(c):
+    M, K, N = (int(v) for v in c["shape"])
+    w = repack(c["w"], M, K)
+    xq, xd = quantize(c["x"], K, N)
+    y = gemv(w, M, K, xq, xd, N, hip.MODE_FAST).reshape(N, M)
+    xq_aos = torch.empty_like(xq)
+    hip.check(hip.lib().vsim_op_q4_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
+    exact, absum = _fp64_product(c["w"], M, K, host(xq_aos), N)
+    # tolerance: |y - y64| <= 4*K*2^-24 * sum|w_i x_i| (fp32 accumulation bound, well above
+    # the observed error); the reference's own chain meets the same bound
+    tol = 4.0 * K * 2.0 ** -24 * absum + 1e-30
+    assert np.all(np.abs(y - exact) <= tol)
+    assert np.all(np.abs(c["y"].reshape(N, M) - exact) <= tol)
+
+
+def test_gemv_bias_epilogue():
+    rng = np.random.default_rng(3)
+    M, K = 256, 512
+    aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))
+    b = rng.standard_normal(M).astype(np.float32)
+    w = repack(aos, M, K)
+    xq, xd = quantize(rng.standard_normal(K).astype(np.float32), K, 1)
+    y0 = gemv(w, M, K, xq, xd, 1, hip.MODE_EXACT)
+    y1 = gemv(w, M, K, xq, xd, 1, hip.MODE_EXACT, bias=dev(b))
+    assert np.array_equal(bits(y1), bits((y0 + b).astype(np.float32)))
+
+
+@pytest.mark.parametrize("c", cases(ops("norm")), ids=lambda c: "x".join(map(str, c["shape"])))
+def test_norm_bit_exact(c):
+    n, r = (int(v) for v in c["shape"])
+    x = dev(c["x"])
+    y = torch.empty_like(x)
+    hip.check(hip.lib().vsim_op_norm(x.data_ptr(), y.data_ptr(), n, r, None, None, None), "norm")
+    assert np.array_equal(bits(host(y)), bits(c["y"]))
+
+
+def test_norm_fallback_paths():
+    """Rows built to defeat both fast-path certificates must still match the oracle."""
+    import oracle_py as O
+    rng = np.random.default_rng(11)
+    n = 4096
+    rows = []
+    r0 = rng.standard_normal(n).astype(np.float32) * 100
+    r0[::7] = np.float32(1e-30)  # tiny values: mean sum not provably exact
+    rows.append(r0)
+    r1 = np.full(n, 3.0, np.float32) + rng.standard_normal(n).astype(np.float32) * np.float32(1e-6)
+    rows.append(r1)  # near-constant row: variance tiny
+    x = np.concatenate(rows).astype(np.float32)
+    ref = O.norm(x, n, len(rows))
+    xt = dev(x)
+    y = torch.empty_like(xt)
+    hip.check(hip.lib().vsim_op_norm(xt.data_ptr(), y.data_ptr(), n, len(rows), None, None, None), "norm")
+    assert np.array_equal(bits(host(y)), bits(ref))
+
+
+def test_gelu_bit_exact():
+    z = ops("gelu")
+    x = dev(z["x"])
+    y = torch.empty_like(x)
+    hip.check(hip.lib().vsim_op_gelu(x.data_ptr(), y.data_ptr(), x.numel(), None), "gelu")
+    assert np.array_equal(bits(host(y)), bits(z["y"]))
+
+
+@pytest.mark.parametrize("c", cases(ops("attnsm")), ids=lambda c: "x".join(map(str, c["shape"])))
+def test_scale_mask_softmax_bit_exact(c):
+    nc, nr, nz, n_past = (int(v) for v in c["shape"])
+    p = dev(c["x"])
+    hip.check(hip.lib().vsim_op_attn_softmax(p.data_ptr(), nc, nr, nz, n_past, float(c["scale"][0]), None), "sm")
+    assert np.array_equal(bits(host(p)), bits(c["y"]))
+
+
+@pytest.mark.parametrize("style", [0, 1], ids=["neox", "gptj"])
+def test_rope_bit_exact(style):
+    for c in cases(ops("rope_neox" if style == 0 else "rope_gptj")):
+        d, H, T, n_past, n_dims, mode = (int(v) for v in c["shape"])
+        x = dev(c["x"])
+        hip.check(hip.lib().vsim_op_rope(style, x.data_ptr(), d, H, T, n_past, n_dims, mode, None), "rope")
+        assert np.array_equal(bits(host(x)), bits(c["y"])), c["shape"]
+
+
+def test_kq_bit_exact():
+    for c in cases(ops("kq")):
+        d, H, nk, N = (int(v) for v in c["shape"])
+        K, Q = dev(c["a"]), dev(c["b"])
+        out = torch.empty(H * N * nk, dtype=torch.float32, device=DEV)
+        hip.check(hip.lib().vsim_op_kq(K.data_ptr(), d * H, Q.data_ptr(), d * H, d, H, nk, N, out.data_ptr(), None),
+                  "kq")
+        assert np.array_equal(bits(host(out)), bits(c["y"])), c["shape"]
+
+
+def test_kqv_bit_exact():
+    for c in cases(ops("kqv")):
+        d, H, nk, N = (int(v) for v in c["shape"])
+        V, S = dev(c["a"]), dev(c["b"])
+        out = torch.empty(H * N * d, dtype=torch.float32, device=DEV)
+        hip.check(hip.lib().vsim_op_kqv(V.data_ptr(), d * H, S.data_ptr(), d, H, nk, N, out.data_ptr(), None), "kqv")
+        assert np.array_equal(bits(host(out)), bits(c["y"])), c["shape"]
+
+
+def test_get_rows_bit_exact():
+    z = ops("getrows")
+    K, V = (int(v) for v in z["shape"])
+    w = repack(z["w"], V, K)
+    idx = dev(z["idx"])
+    y = torch.empty(idx.numel() * K, dtype=torch.float32, device=DEV)
+    hip.check(hip.lib().vsim_op_get_rows(w.data_ptr(), K, V, idx.data_ptr(), idx.numel(), y.data_ptr(), None), "rows")
+    assert np.array_equal(bits(host(y)), bits(z["y"]))
+
+
+@pytest.mark.parametrize("M,K", [(4096, 4096), (1024, 16384), (50400, 256)])
+def test_gemv_exact_full_width_vs_oracle(M, K):
+    """GPT-J widths (K = n_embd and 4*n_embd, V rows) against the CPU restatement."""
+    import oracle_py as O
+    rng = np.random.default_rng(M + K)
+    aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))
+    x = rng.standard_normal(K).astype(np.float32)
+    ref = O.mul_mat(aos, M, K, x, 1, nthreads=8)
+    w = repack(aos, M, K)
+    xq, xd = quantize(x, K, 1)
+    assert np.array_equal(bits(gemv(w, M, K, xq, xd, 1, hip.MODE_EXACT)), bits(ref))

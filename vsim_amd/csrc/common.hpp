@@ -1,0 +1,133 @@
+// vsim_amd/csrc/common.hpp — shared device helpers and launch declarations.
+//
+// Every translation unit is compiled with -ffp-contract=off: the reference's x86 build
+// (-O2 -msse3, Makefile-ubuntu:5-6) never fuses a multiply into an add, and the exact
+// kernels must round every product and sum exactly where the reference does.  Fast
+// kernels that want FMA call __builtin_fmaf explicitly.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace vsim {
+
+constexpr int QK = 32;       // weights per Q4_0 block (ggml.c:204)
+constexpr int QBYTES = 20;   // fp32 d + 16 nibble bytes (ggml.c:907-909)
+
+// ---------------------------------------------------------------- Q4 SoA views
+// Device layout of a Q4_0 matrix: nibble plane qs[rows][nb][16], then scale plane
+// d[rows][nb] (fp32).  Same 0.625 B/weight as the ggml AoS block.
+struct Q4View {
+  const uint8_t *qs;
+  const float *d;
+  int rows, k;
+  __host__ __device__ int nb() const { return k / QK; }
+};
+
+inline Q4View q4_view(const void *base, int rows, int k) {
+  const size_t nb = (size_t)k / QK;
+  Q4View v;
+  v.qs = (const uint8_t *)base;
+  v.d = (const float *)((const uint8_t *)base + (size_t)rows * nb * 16);
+  v.rows = rows;
+  v.k = k;
+  return v;
+}
+
+// ---------------------------------------------------------------- fp16 (ggml.c:95-142)
+__device__ __forceinline__ float bits_f(uint32_t w) { return __uint_as_float(w); }
+__device__ __forceinline__ uint32_t f_bits(float f) { return __float_as_uint(f); }
+
+__device__ __forceinline__ float h2f(uint16_t h) {
+  const uint32_t w = (uint32_t)h << 16;
+  const uint32_t sign = w & 0x80000000u;
+  const uint32_t two_w = w + w;
+  const float normalized = bits_f((two_w >> 4) + (0xE0u << 23)) * 0x1.0p-112f;
+  const float denormalized = bits_f((two_w >> 17) | (126u << 23)) - 0.5f;
+  return bits_f(sign | (two_w < (1u << 27) ? f_bits(denormalized) : f_bits(normalized)));
+}
+
+__device__ __forceinline__ uint16_t f2h(float f) {
+  float base = (fabsf(f) * 0x1.0p+112f) * 0x1.0p-110f;
+  const uint32_t w = f_bits(f);
+  const uint32_t shl1_w = w + w;
+  const uint32_t sign = w & 0x80000000u;
+  uint32_t bias = shl1_w & 0xFF000000u;
+  if (bias < 0x71000000u) bias = 0x71000000u;
+  base = bits_f((bias >> 1) + 0x07800000u) + base;
+  const uint32_t bits = f_bits(base);
+  const uint32_t exp_bits = (bits >> 13) & 0x00007C00u;
+  const uint32_t mantissa_bits = bits & 0x00000FFFu;
+  const uint32_t nonsign = exp_bits + mantissa_bits;
+  return (uint16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+
+// ---------------------------------------------------------------- wave reductions
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string &msg);
+int hip_fail(hipError_t e, const char *what);
+#define VSIM_HIP(call)                                          \
+  do {                                                          \
+    hipError_t e_ = (call);                                     \
+    if (e_ != hipSuccess) return ::vsim::hip_fail(e_, #call);   \
+  } while (0)
+
+// ---------------------------------------------------------------- launchers (ops_*.hip)
+// All return 0 / negative VSIM_E*; all enqueue on `s` and never synchronise.
+struct DevTables {
+  const uint16_t *exp_f16;   // table_exp_f16 (ggml.c:1249)
+  const uint16_t *gelu_f16;  // table_gelu_f16 (ggml.c:1247)
+};
+int tables_get(DevTables *t);  // lazily uploads host-built tables for the current device
+
+int launch_q4_repack(const void *aos, void *soa, int rows, int k, hipStream_t s);
+int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s);
+int launch_q4_quantize(const float *x, int k, int n, void *xq, float *xd, hipStream_t s);
+int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias,
+                   float *y, int mode, hipStream_t s);
+int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s);
+int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
+int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
+int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s);
+int launch_rope(int style, float *x, int d, int H, int T, int n_past, int n_dims, int mode,
+                const double2 *cs, hipStream_t s);
+int launch_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq,
+              hipStream_t s);
+int launch_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, int merged,
+               hipStream_t s);
+int launch_rope_kv_write(int style, float *Q, const float *K, const float *V, float *kcache, float *vcache,
+                         int d, int H, int N, int n_past, int n_dims, const double2 *cs, hipStream_t s);
+int launch_add_residual(float *inpL, const float *attn, const float *ff, int n, int order_ff_first,
+                        hipStream_t s);
+int launch_add_bias(float *x, const float *b, int k, int n, hipStream_t s);
+int launch_randn_q4(void *soa, int rows, int k, uint64_t seed, float stddev, hipStream_t s);
+int launch_randn_f32(float *x, int n, uint64_t seed, float stddev, float mean, hipStream_t s);
+
+// host-side: cos/sin table of the reference RoPE angles (ggml.c:6117-6120 / 5952-5955),
+// cs[p*(n_dims/2) + j] = {cos(p*theta_j), sin(p*theta_j)}, theta_j = 10000^(-2j/n_dims)
+void rope_table_host(double2 *cs, int n_pos, int n_dims);
+
+}  // namespace vsim

@@ -1,0 +1,622 @@
+// vsim_amd/csrc/model.cpp — device-resident model executor (layer 3 of vsim_hip.h).
+//
+// One eval = the reference's gptneox_eval graph (vsim.cpp:470-747) or the GPT-J graph
+// built from the same ggml ops, executed as a fixed sequence of HIP kernels on one
+// stream.  Weights (Q4 SoA), LayerNorm/bias vectors, the F32 KV cache
+// ([layer][n_ctx][E], vsim.cpp:349-366) and all activations stay in HBM; per eval the
+// host sends the token ids and receives one logits row (vsim.cpp:736-737).
+// A pipeline stage owns layers [l0, l1); stages exchange the residual inpL ([N][E] f32).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "../../include/vsim_hip.h"
+
+using namespace vsim;
+
+namespace {
+
+enum Kind { KQ4 = 0, KF32 = 1 };
+
+struct Slot {
+  void *ptr;
+  int kind;
+  int rows, k;  // Q4: rows x k ; F32: k elements (rows = 1)
+  int layer;    // -1 for global tensors
+  bool loaded;
+};
+
+struct LayerW {
+  void *wq = nullptr, *wk = nullptr, *wv = nullptr, *wo = nullptr, *wfc = nullptr, *wproj = nullptr;
+  float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+  float *bq = nullptr, *bk = nullptr, *bv = nullptr, *bo = nullptr, *bfc = nullptr, *bproj = nullptr;
+};
+
+}  // namespace
+
+struct vsim_model {
+  int arch = VSIM_ARCH_GPTNEOX;
+  vsim_hparams hp{};
+  int n_ctx = 512, device = 0, l0 = 0, l1 = 0;
+  bool first = true, last = true;
+  int mode = VSIM_MODE_EXACT;
+  bool graph_enabled = false;
+  hipStream_t stream = nullptr;
+
+  uint8_t *warena = nullptr;  // all weights of this stage
+  size_t wbytes = 0;
+  std::map<std::string, Slot> slots;
+  std::vector<LayerW> layers;
+  void *wte = nullptr, *lmh = nullptr;
+  float *lnf_w = nullptr, *lnf_b = nullptr, *lmh_b = nullptr;
+
+  float *kcache = nullptr, *vcache = nullptr;
+  double2 *rope_cs = nullptr;
+
+  // scratch, sized for n_max tokens
+  int n_max = 0;
+  float *inpL = nullptr, *cur1 = nullptr, *cur2 = nullptr, *Qb = nullptr, *Kb = nullptr, *Vb = nullptr;
+  float *attn_in = nullptr, *attn = nullptr, *ff = nullptr, *fch = nullptr, *kq = nullptr, *logits = nullptr;
+  uint8_t *xq1 = nullptr, *xq2 = nullptr, *xq3 = nullptr;
+  float *xd1 = nullptr, *xd2 = nullptr, *xd3 = nullptr;
+  int32_t *tok_dev = nullptr;
+  int32_t *tok_host = nullptr;  // pinned
+  float *logit_host = nullptr;  // pinned
+  int kernels_last = 0;
+
+  // GEMV profiling (bench.py's live roofline): event pair around every GEMV launch
+  bool profile = false;
+  std::vector<hipEvent_t> prof_events;
+  size_t prof_used = 0;
+  double prof_ms = 0.0, prof_bytes = 0.0;
+  long prof_launches = 0;
+};
+
+namespace {
+
+int E_(const vsim_model *m) { return m->hp.n_embd; }
+
+void free_scratch(vsim_model *m) {
+  void *ps[] = {m->inpL, m->cur1, m->cur2, m->Qb, m->Kb, m->Vb, m->attn_in, m->attn, m->ff, m->fch, m->kq,
+                m->logits, m->xq1, m->xq2, m->xq3, m->xd1, m->xd2, m->xd3, m->tok_dev};
+  for (void *p : ps)
+    if (p) (void)hipFree(p);
+  if (m->tok_host) (void)hipHostFree(m->tok_host);
+  if (m->logit_host) (void)hipHostFree(m->logit_host);
+  m->inpL = m->cur1 = m->cur2 = m->Qb = m->Kb = m->Vb = m->attn_in = m->attn = m->ff = m->fch = m->kq = m->logits =
+      nullptr;
+  m->xq1 = m->xq2 = m->xq3 = nullptr;
+  m->xd1 = m->xd2 = m->xd3 = nullptr;
+  m->tok_dev = nullptr;
+  m->tok_host = nullptr;
+  m->logit_host = nullptr;
+  m->n_max = 0;
+}
+
+int ensure_scratch(vsim_model *m, int N) {
+  if (N <= m->n_max) return VSIM_OK;
+  VSIM_HIP(hipStreamSynchronize(m->stream));
+  free_scratch(m);
+  const int n = N < 16 ? 16 : N;
+  const size_t E = E_(m), F = 4 * E, V = m->hp.n_vocab, H = m->hp.n_head;
+  auto fa = [&](float **p, size_t cnt) { return hipMalloc((void **)p, cnt * sizeof(float)); };
+  auto ba = [&](uint8_t **p, size_t k) { return hipMalloc((void **)p, (size_t)n * k / QK * QBYTES); };
+  VSIM_HIP(fa(&m->inpL, n * E));
+  VSIM_HIP(fa(&m->cur1, n * E));
+  VSIM_HIP(fa(&m->cur2, n * E));
+  VSIM_HIP(fa(&m->Qb, n * E));
+  VSIM_HIP(fa(&m->Kb, n * E));
+  VSIM_HIP(fa(&m->Vb, n * E));
+  VSIM_HIP(fa(&m->attn_in, n * E));
+  VSIM_HIP(fa(&m->attn, n * E));
+  VSIM_HIP(fa(&m->ff, n * E));
+  VSIM_HIP(fa(&m->fch, n * F));
+  VSIM_HIP(fa(&m->kq, (size_t)n * H * m->n_ctx));
+  VSIM_HIP(fa(&m->logits, V));
+  VSIM_HIP(ba(&m->xq1, E));
+  VSIM_HIP(ba(&m->xq2, E));
+  VSIM_HIP(ba(&m->xq3, F));
+  VSIM_HIP(fa(&m->xd1, n * E));
+  VSIM_HIP(fa(&m->xd2, n * E));
+  VSIM_HIP(fa(&m->xd3, n * F));
+  VSIM_HIP(hipMalloc((void **)&m->tok_dev, n * sizeof(int32_t)));
+  VSIM_HIP(hipHostMalloc((void **)&m->tok_host, n * sizeof(int32_t), hipHostMallocDefault));
+  VSIM_HIP(hipHostMalloc((void **)&m->logit_host, V * sizeof(float), hipHostMallocDefault));
+  m->n_max = n;
+  return VSIM_OK;
+}
+
+// Register every tensor this stage owns, with its ggml-file name and byte size.
+void plan_slots(vsim_model *m, std::vector<std::pair<std::string, Slot>> &out) {
+  const int E = m->hp.n_embd, V = m->hp.n_vocab, F = 4 * E;
+  auto q = [&](const std::string &n, int rows, int k, int layer) { out.push_back({n, Slot{nullptr, KQ4, rows, k, layer, false}}); };
+  auto f = [&](const std::string &n, int k, int layer) { out.push_back({n, Slot{nullptr, KF32, 1, k, layer, false}}); };
+  if (m->arch == VSIM_ARCH_GPTNEOX) {
+    if (m->first) q("gpt_neox.embed_in.weight", V, E, -1);
+    if (m->last) {
+      f("gpt_neox.final_layer_norm.weight", E, -1);
+      f("gpt_neox.final_layer_norm.bias", E, -1);
+      q("embed_out.weight", V, E, -1);
+    }
+    for (int i = m->l0; i < m->l1; ++i) {
+      const std::string p = "gpt_neox.layers." + std::to_string(i) + ".";
+      f(p + "input_layernorm.weight", E, i);
+      f(p + "input_layernorm.bias", E, i);
+      f(p + "post_attention_layernorm.weight", E, i);
+      f(p + "post_attention_layernorm.bias", E, i);
+      q(p + "attention.query.weight", E, E, i);
+      f(p + "attention.query.bias", E, i);
+      q(p + "attention.key.weight", E, E, i);
+      f(p + "attention.key.bias", E, i);
+      q(p + "attention.value.weight", E, E, i);
+      f(p + "attention.value.bias", E, i);
+      q(p + "attention.dense.weight", E, E, i);
+      f(p + "attention.dense.bias", E, i);
+      q(p + "mlp.dense_h_to_4h.weight", F, E, i);
+      f(p + "mlp.dense_h_to_4h.bias", F, i);
+      q(p + "mlp.dense_4h_to_h.weight", E, F, i);
+      f(p + "mlp.dense_4h_to_h.bias", E, i);
+    }
+  } else {
+    if (m->first) q("transformer.wte.weight", V, E, -1);
+    if (m->last) {
+      f("transformer.ln_f.weight", E, -1);
+      f("transformer.ln_f.bias", E, -1);
+      q("lm_head.weight", V, E, -1);
+      f("lm_head.bias", V, -1);
+    }
+    for (int i = m->l0; i < m->l1; ++i) {
+      const std::string p = "transformer.h." + std::to_string(i) + ".";
+      f(p + "ln_1.weight", E, i);
+      f(p + "ln_1.bias", E, i);
+      q(p + "attn.q_proj.weight", E, E, i);
+      q(p + "attn.k_proj.weight", E, E, i);
+      q(p + "attn.v_proj.weight", E, E, i);
+      q(p + "attn.out_proj.weight", E, E, i);
+      q(p + "mlp.fc_in.weight", F, E, i);
+      f(p + "mlp.fc_in.bias", F, i);
+      q(p + "mlp.fc_out.weight", E, F, i);
+      f(p + "mlp.fc_out.bias", E, i);
+    }
+  }
+}
+
+size_t slot_bytes(const Slot &s) {
+  return s.kind == KQ4 ? (size_t)s.rows * s.k / QK * QBYTES : (size_t)s.k * sizeof(float);
+}
+
+void bind_pointers(vsim_model *m) {
+  auto P = [&](const std::string &n) -> void * {
+    auto it = m->slots.find(n);
+    return it == m->slots.end() ? nullptr : it->second.ptr;
+  };
+  auto F = [&](const std::string &n) { return (float *)P(n); };
+  m->layers.assign(m->l1 - m->l0, LayerW{});
+  if (m->arch == VSIM_ARCH_GPTNEOX) {
+    m->wte = P("gpt_neox.embed_in.weight");
+    m->lnf_w = F("gpt_neox.final_layer_norm.weight");
+    m->lnf_b = F("gpt_neox.final_layer_norm.bias");
+    m->lmh = P("embed_out.weight");
+    for (int i = m->l0; i < m->l1; ++i) {
+      LayerW &L = m->layers[i - m->l0];
+      const std::string p = "gpt_neox.layers." + std::to_string(i) + ".";
+      L.ln1_w = F(p + "input_layernorm.weight");
+      L.ln1_b = F(p + "input_layernorm.bias");
+      L.ln2_w = F(p + "post_attention_layernorm.weight");
+      L.ln2_b = F(p + "post_attention_layernorm.bias");
+      L.wq = P(p + "attention.query.weight");
+      L.bq = F(p + "attention.query.bias");
+      L.wk = P(p + "attention.key.weight");
+      L.bk = F(p + "attention.key.bias");
+      L.wv = P(p + "attention.value.weight");
+      L.bv = F(p + "attention.value.bias");
+      L.wo = P(p + "attention.dense.weight");
+      L.bo = F(p + "attention.dense.bias");
+      L.wfc = P(p + "mlp.dense_h_to_4h.weight");
+      L.bfc = F(p + "mlp.dense_h_to_4h.bias");
+      L.wproj = P(p + "mlp.dense_4h_to_h.weight");
+      L.bproj = F(p + "mlp.dense_4h_to_h.bias");
+    }
+  } else {
+    m->wte = P("transformer.wte.weight");
+    m->lnf_w = F("transformer.ln_f.weight");
+    m->lnf_b = F("transformer.ln_f.bias");
+    m->lmh = P("lm_head.weight");
+    m->lmh_b = F("lm_head.bias");
+    for (int i = m->l0; i < m->l1; ++i) {
+      LayerW &L = m->layers[i - m->l0];
+      const std::string p = "transformer.h." + std::to_string(i) + ".";
+      L.ln1_w = F(p + "ln_1.weight");
+      L.ln1_b = F(p + "ln_1.bias");
+      L.wq = P(p + "attn.q_proj.weight");
+      L.wk = P(p + "attn.k_proj.weight");
+      L.wv = P(p + "attn.v_proj.weight");
+      L.wo = P(p + "attn.out_proj.weight");
+      L.wfc = P(p + "mlp.fc_in.weight");
+      L.bfc = F(p + "mlp.fc_in.bias");
+      L.wproj = P(p + "mlp.fc_out.weight");
+      L.bproj = F(p + "mlp.fc_out.bias");
+    }
+  }
+}
+
+#define RC(x)                    \
+  do {                           \
+    int rc_ = (x);               \
+    if (rc_) return rc_;         \
+  } while (0)
+
+// Quantize an activation and run one GEMV in the model's mode.
+int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_t *xq, float *xd, bool quantize,
+       const float *bias, float *y, int &nk) {
+  if (quantize) {
+    RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
+    ++nk;
+  }
+  hipEvent_t *ev = nullptr;
+  if (m->profile) {
+    if (m->prof_used + 2 > m->prof_events.size()) {
+      hipEvent_t a, b;
+      VSIM_HIP(hipEventCreate(&a));
+      VSIM_HIP(hipEventCreate(&b));
+      m->prof_events.push_back(a);
+      m->prof_events.push_back(b);
+    }
+    ev = &m->prof_events[m->prof_used];
+    m->prof_used += 2;
+    VSIM_HIP(hipEventRecord(ev[0], m->stream));
+  }
+  RC(launch_q4_gemv(W, M, K, xq, xd, N, bias, y, m->mode, m->stream));
+  if (ev) {
+    VSIM_HIP(hipEventRecord(ev[1], m->stream));
+    m->prof_bytes += (double)M * K / QK * QBYTES;
+  }
+  ++nk;
+  return VSIM_OK;
+}
+
+int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
+  const LayerW &L = m->layers[il - m->l0];
+  const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E;
+  const bool gptj = m->arch == VSIM_ARCH_GPTJ;
+  hipStream_t s = m->stream;
+  // input LayerNorm + affine (vsim.cpp:526-533)
+  RC(launch_norm(m->inpL, m->cur1, E, N, L.ln1_w, L.ln1_b, s)); ++nk;
+  // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
+  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk));
+  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, m->Kb, nk));
+  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, m->Vb, nk));
+  // KV write + RoPE (vsim.cpp:553-580)
+  const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
+  float *kc = m->kcache + loff, *vc = m->vcache + loff;
+  RC(launch_rope_kv_write(gptj ? 1 : 0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, m->hp.n_rot, m->rope_cs, s)); ++nk;
+  // attention (vsim.cpp:583-616)
+  const int nkv = n_past + N;
+  const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
+  RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
+  RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
+  RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, gptj ? nullptr : L.bo, m->attn, nk));
+  // feed-forward input
+  const uint8_t *fxq = m->xq1;
+  const float *fxd = m->xd1;
+  bool fquant = false;
+  const float *fx = m->cur1;
+  if (!gptj) {
+    if (m->hp.use_parallel_residual) {
+      RC(launch_norm(m->inpL, m->cur2, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
+    } else {
+      // inpFF = cur + inpL ; norm ; affine  (vsim.cpp:631-649)
+      VSIM_HIP(hipMemcpyAsync(m->cur2, m->attn, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+      RC(launch_add_bias(m->cur2, m->inpL, N * E, 1, s)); ++nk;  // cur + inpL elementwise
+      RC(launch_norm(m->cur2, m->cur2, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
+    }
+    fx = m->cur2;
+    fxq = m->xq2;
+    fxd = m->xd2;
+    fquant = true;
+  }
+  RC(mm(m, L.wfc, F, E, fx, N, (uint8_t *)fxq, (float *)fxd, fquant, nullptr, m->fch, nk));
+  RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
+  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk));
+  RC(launch_add_residual(m->inpL, m->attn, m->ff, N * E, (!gptj && !m->hp.use_parallel_residual) ? 1 : 0, s)); ++nk;
+  return VSIM_OK;
+}
+
+thread_local std::string t_err;
+
+}  // namespace
+
+namespace vsim {
+void set_error(const std::string &msg) { t_err = msg; }
+int hip_fail(hipError_t e, const char *what) {
+  t_err = std::string(what) + ": " + hipGetErrorString(e);
+  return VSIM_EHIP;
+}
+}  // namespace vsim
+
+extern "C" {
+
+const char *vsim_last_error(void) { return t_err.c_str(); }
+
+int vsim_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+size_t vsim_q4_bytes(int rows, int k) { return (size_t)rows * k / QK * QBYTES; }
+
+int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
+                      vsim_model **out) {
+  if (!hp || !out) { set_error("model_create: null argument"); return VSIM_EINVAL; }
+  if (arch != VSIM_ARCH_GPTNEOX && arch != VSIM_ARCH_GPTJ) { set_error("model_create: unknown arch"); return VSIM_EINVAL; }
+  if (hp->n_embd % hp->n_head || hp->n_embd % 128 || hp->n_rot > hp->n_embd / hp->n_head || hp->n_rot % 2 ||
+      n_ctx <= 0) {
+    set_error("model_create: unsupported hparams (n_embd % 128, n_rot <= head dim, even n_rot)");
+    return VSIM_EINVAL;
+  }
+  if (layer_end < 0) layer_end = hp->n_layer;
+  if (layer_begin < 0 || layer_begin >= layer_end || layer_end > hp->n_layer) {
+    set_error("model_create: bad layer range");
+    return VSIM_EINVAL;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) { set_error("model_create: no such device"); return VSIM_ENODEV; }
+  VSIM_HIP(hipSetDevice(device));
+  auto *m = new vsim_model();
+  m->arch = arch;
+  m->hp = *hp;
+  m->n_ctx = n_ctx;
+  m->device = device;
+  m->l0 = layer_begin;
+  m->l1 = layer_end;
+  m->first = layer_begin == 0;
+  m->last = layer_end == hp->n_layer;
+  auto fail = [&](int rc) { vsim_model_free(m); return rc; };
+  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) return fail(hip_fail(hipErrorUnknown, "stream"));
+  std::vector<std::pair<std::string, Slot>> plan;
+  plan_slots(m, plan);
+  size_t tot = 0;
+  for (auto &ps : plan) tot += (slot_bytes(ps.second) + 255) & ~(size_t)255;
+  if (hipMalloc((void **)&m->warena, tot) != hipSuccess) { set_error("model_create: weight alloc failed"); return fail(VSIM_ENOMEM); }
+  m->wbytes = tot;
+  size_t off = 0;
+  for (auto &ps : plan) {
+    ps.second.ptr = m->warena + off;
+    off += (slot_bytes(ps.second) + 255) & ~(size_t)255;
+    m->slots[ps.first] = ps.second;
+  }
+  bind_pointers(m);
+  const size_t E = hp->n_embd, nl = layer_end - layer_begin;
+  if (hipMalloc((void **)&m->kcache, nl * n_ctx * E * sizeof(float)) != hipSuccess ||
+      hipMalloc((void **)&m->vcache, nl * n_ctx * E * sizeof(float)) != hipSuccess) {
+    set_error("model_create: KV cache alloc failed");
+    return fail(VSIM_ENOMEM);
+  }
+  (void)hipMemset(m->kcache, 0, nl * n_ctx * E * sizeof(float));
+  (void)hipMemset(m->vcache, 0, nl * n_ctx * E * sizeof(float));
+  const int half = hp->n_rot / 2 > 0 ? hp->n_rot / 2 : 1;
+  std::vector<double2> cs((size_t)n_ctx * half);
+  if (hp->n_rot > 0) rope_table_host(cs.data(), n_ctx, hp->n_rot);
+  if (hipMalloc((void **)&m->rope_cs, cs.size() * sizeof(double2)) != hipSuccess) return fail(VSIM_ENOMEM);
+  if (hipMemcpy(m->rope_cs, cs.data(), cs.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(hip_fail(hipErrorUnknown, "rope table upload"));
+  DevTables t;
+  if (int rc = tables_get(&t)) return fail(rc);
+  if (int rc = ensure_scratch(m, 16)) return fail(rc);
+  *out = m;
+  return VSIM_OK;
+}
+
+void vsim_model_free(vsim_model *m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  if (m->stream) (void)hipStreamSynchronize(m->stream);
+  free_scratch(m);
+  if (m->warena) (void)hipFree(m->warena);
+  if (m->kcache) (void)hipFree(m->kcache);
+  if (m->vcache) (void)hipFree(m->vcache);
+  if (m->rope_cs) (void)hipFree(m->rope_cs);
+  if (m->stream) (void)hipStreamDestroy(m->stream);
+  delete m;
+}
+
+int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes) {
+  auto it = m->slots.find(name);
+  if (it == m->slots.end()) { set_error(std::string("set_tensor: unknown tensor ") + name); return VSIM_EINVAL; }
+  Slot &s = it->second;
+  if (nbytes != slot_bytes(s)) { set_error(std::string("set_tensor: wrong size for ") + name); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  if (s.kind == KF32) {
+    VSIM_HIP(hipMemcpy(s.ptr, host, nbytes, hipMemcpyHostToDevice));
+  } else {
+    void *stage = nullptr;
+    VSIM_HIP(hipMalloc(&stage, nbytes));
+    hipError_t e = hipMemcpy(stage, host, nbytes, hipMemcpyHostToDevice);
+    int rc = e == hipSuccess ? launch_q4_repack(stage, s.ptr, s.rows, s.k, m->stream) : hip_fail(e, "upload");
+    if (rc == 0) rc = hipStreamSynchronize(m->stream) == hipSuccess ? 0 : VSIM_EHIP;
+    (void)hipFree(stage);
+    if (rc) return rc;
+  }
+  s.loaded = true;
+  return VSIM_OK;
+}
+
+int vsim_model_randomize(vsim_model *m, uint64_t seed, float stddev) {
+  VSIM_HIP(hipSetDevice(m->device));
+  uint64_t id = 0;
+  for (auto &kv : m->slots) {
+    Slot &s = kv.second;
+    const uint64_t sd = seed * 0x9E3779B97F4A7C15ull + (++id) * 0xD1B54A32D192ED03ull;
+    const bool gain = kv.first.find("norm.weight") != std::string::npos || kv.first.find("ln_") != std::string::npos
+                          ? kv.first.find(".weight") != std::string::npos
+                          : false;
+    if (s.kind == KQ4)
+      RC(launch_randn_q4(s.ptr, s.rows, s.k, sd, stddev, m->stream));
+    else
+      RC(launch_randn_f32((float *)s.ptr, s.k, sd, stddev, gain ? 1.0f : 0.0f, m->stream));
+    s.loaded = true;
+  }
+  VSIM_HIP(hipStreamSynchronize(m->stream));
+  return VSIM_OK;
+}
+
+int vsim_model_load_file(const char *path, int arch, int n_ctx, int device, int layer_begin, int layer_end,
+                         vsim_model **out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) { set_error(std::string("load: cannot open ") + path); return VSIM_EFILE; }
+  auto rd = [&](void *p, size_t n) { f.read((char *)p, n); return (size_t)f.gcount() == n; };
+  uint32_t magic = 0;
+  if (!rd(&magic, 4) || magic != 0x67676d6c) { set_error("load: bad magic"); return VSIM_EFILE; }
+  vsim_hparams hp{};
+  int32_t ftype = 0;
+  rd(&hp.n_vocab, 4); rd(&hp.n_embd, 4); rd(&hp.n_head, 4); rd(&hp.n_layer, 4); rd(&hp.n_rot, 4);
+  hp.use_parallel_residual = 1;
+  if (arch == VSIM_ARCH_GPTNEOX) rd(&hp.use_parallel_residual, 4);
+  rd(&ftype, 4);
+  if (ftype != 2) { set_error("load: only Q4_0 (f16 == 2) files are supported"); return VSIM_EFILE; }
+  int32_t nv = hp.n_vocab;
+  if (arch == VSIM_ARCH_GPTJ) rd(&nv, 4);
+  for (int i = 0; i < nv; ++i) {
+    uint32_t len = 0;
+    if (!rd(&len, 4)) { set_error("load: truncated vocab"); return VSIM_EFILE; }
+    f.seekg(len, std::ios::cur);
+  }
+  vsim_model *m = nullptr;
+  if (layer_end < 0) layer_end = hp.n_layer;
+  RC(vsim_model_create(arch, &hp, n_ctx, device, layer_begin, layer_end, &m));
+  std::vector<char> buf;
+  while (true) {
+    int32_t nd = 0, ln = 0, ft = 0;
+    if (!rd(&nd, 4)) break;
+    rd(&ln, 4);
+    rd(&ft, 4);
+    size_t ne = 1;
+    int32_t dims[4] = {1, 1, 1, 1};
+    for (int i = 0; i < nd && i < 4; ++i) { rd(&dims[i], 4); ne *= dims[i]; }
+    std::string name(ln, 0);
+    rd(&name[0], ln);
+    const size_t nbytes = ft == 0 ? ne * 4 : (ft == 2 ? ne / QK * QBYTES : 0);
+    if (nbytes == 0) { vsim_model_free(m); set_error("load: unsupported tensor type in " + name); return VSIM_EFILE; }
+    auto it = m->slots.find(name);
+    if (it == m->slots.end()) {  // tensor of another pipeline stage
+      f.seekg(nbytes, std::ios::cur);
+      continue;
+    }
+    buf.resize(nbytes);
+    if (!rd(buf.data(), nbytes)) { vsim_model_free(m); set_error("load: truncated tensor " + name); return VSIM_EFILE; }
+    if ((it->second.kind == KQ4) != (ft == 2)) { vsim_model_free(m); set_error("load: type mismatch " + name); return VSIM_EFILE; }
+    if (int rc = vsim_model_set_tensor(m, name.c_str(), buf.data(), nbytes)) { vsim_model_free(m); return rc; }
+  }
+  for (auto &kv : m->slots)
+    if (!kv.second.loaded) {
+      std::string n = kv.first;
+      vsim_model_free(m);
+      set_error("load: tensor missing from file: " + n);
+      return VSIM_EFILE;
+    }
+  *out = m;
+  return VSIM_OK;
+}
+
+int vsim_model_set_mode(vsim_model *m, int mode) {
+  if (mode != VSIM_MODE_EXACT && mode != VSIM_MODE_FAST) { set_error("set_mode: bad mode"); return VSIM_EINVAL; }
+  m->mode = mode;
+  return VSIM_OK;
+}
+
+int vsim_model_set_graph(vsim_model *m, int enable) {
+  m->graph_enabled = enable != 0;
+  return VSIM_OK;
+}
+
+int vsim_model_hparams(const vsim_model *m, vsim_hparams *hp, int *n_ctx, int *lb, int *le) {
+  if (hp) *hp = m->hp;
+  if (n_ctx) *n_ctx = m->n_ctx;
+  if (lb) *lb = m->l0;
+  if (le) *le = m->l1;
+  return VSIM_OK;
+}
+
+void *vsim_model_stream(vsim_model *m) { return (void *)m->stream; }
+const float *vsim_model_logits_dev(vsim_model *m) { return m->logits; }
+
+int vsim_model_info(vsim_model *m, int *kernels_per_eval, int *graph_enabled, size_t *weight_bytes) {
+  if (kernels_per_eval) *kernels_per_eval = m->kernels_last;
+  if (graph_enabled) *graph_enabled = m->graph_enabled ? 1 : 0;
+  if (weight_bytes) *weight_bytes = m->wbytes;
+  return VSIM_OK;
+}
+
+int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, const float *resid_in, float *resid_out,
+                    float *logits) {
+  if (N <= 0 || n_past < 0 || n_past + N > m->n_ctx) { set_error("eval: n_past + N exceeds n_ctx"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, N));
+  const int E = m->hp.n_embd, V = m->hp.n_vocab;
+  hipStream_t s = m->stream;
+  int nk = 0;
+  if (m->first) {
+    if (!tokens) { set_error("eval: first stage needs tokens"); return VSIM_EINVAL; }
+    for (int i = 0; i < N; ++i) {
+      if (tokens[i] < 0 || tokens[i] >= V) { set_error("eval: token id out of range"); return VSIM_EINVAL; }
+      m->tok_host[i] = tokens[i];
+    }
+    VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, N * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    RC(launch_get_rows(m->wte, E, V, m->tok_dev, N, m->inpL, s)); ++nk;
+  } else {
+    if (!resid_in) { set_error("eval: non-first stage needs resid_in"); return VSIM_EINVAL; }
+    VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+  }
+  for (int il = m->l0; il < m->l1; ++il) RC(run_layer(m, il, n_past, N, nk));
+  if (m->last) {
+    // only the last row's logits leave the eval (vsim.cpp:736-737); rows are independent
+    const float *xl = m->inpL + (size_t)(N - 1) * E;
+    RC(launch_norm(xl, m->cur1, E, 1, m->lnf_w, m->lnf_b, s)); ++nk;
+    RC(mm(m, m->lmh, V, E, m->cur1, 1, m->xq1, m->xd1, true, m->arch == VSIM_ARCH_GPTJ ? m->lmh_b : nullptr,
+          m->logits, nk));
+    if (logits) {
+      VSIM_HIP(hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s));
+    }
+  } else if (resid_out) {
+    VSIM_HIP(hipMemcpyAsync(resid_out, m->inpL, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+  }
+  VSIM_HIP(hipStreamSynchronize(s));
+  if (m->last && logits) memcpy(logits, m->logit_host, sizeof(float) * V);
+  m->kernels_last = nk;
+  if (m->profile) {
+    for (size_t i = 0; i + 1 < m->prof_used; i += 2) {
+      float ms = 0.0f;
+      VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[i], m->prof_events[i + 1]));
+      m->prof_ms += ms;
+      m->prof_launches++;
+    }
+    m->prof_used = 0;
+  }
+  return VSIM_OK;
+}
+
+int vsim_model_set_profile(vsim_model *m, int enable) {
+  m->profile = enable != 0;
+  m->prof_ms = m->prof_bytes = 0.0;
+  m->prof_launches = 0;
+  m->prof_used = 0;
+  return VSIM_OK;
+}
+
+int vsim_model_profile_stats(vsim_model *m, double *gemv_ms, long *gemv_launches, double *gemv_bytes) {
+  if (gemv_ms) *gemv_ms = m->prof_ms;
+  if (gemv_launches) *gemv_launches = m->prof_launches;
+  if (gemv_bytes) *gemv_bytes = m->prof_bytes;
+  return VSIM_OK;
+}
+
+}  // extern "C"

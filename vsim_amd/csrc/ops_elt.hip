@@ -1,0 +1,290 @@
+// vsim_amd/csrc/ops_elt.hip — LayerNorm, GELU, bias and residual adds.
+//
+//   ggml_compute_forward_norm_f32  ggml.c:4246-4304 (double mean/variance, eps 1e-5f)
+//   ggml_vec_gelu_f32 (fp16 LUT)   ggml.c:795-803, table ggml.c:1240-1251
+//   add / mul / repeat             ggml.c:3344-3418, 3474-3522, 3809-3847
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+#include "../../include/vsim_hip.h"
+
+namespace vsim {
+
+// ------------------------------------------------------------------ LayerNorm (exact)
+// The reference sums the row sequentially in double.  We sum in parallel and prove the
+// sum equal to the sequential one, falling back to the sequential loop otherwise:
+//  * mean: every partial sum of floats that are multiples of 2^umin is exact in double
+//    while sum|x| < 2^(53+umin), so then any order gives the sequential value;
+//  * variance: sequential and tree sums of w_i = v_i^2 >= 0 differ by at most
+//    (2n+64)*2^-53*sum(w); if both ends of that interval give the same float scale
+//    (the map S -> (float)(1/sqrt(S/n+eps)) is monotone) the scale is the reference's.
+// `stats` (optional) counts fallbacks: [0] mean, [1] variance.
+constexpr int NORM_THREADS = 256;
+
+__device__ __forceinline__ int ulp_exp(float x) {
+  const uint32_t b = __float_as_uint(x) & 0x7FFFFFFFu;
+  if (b == 0) return 1 << 30;
+  const int e = (int)(b >> 23);
+  return e == 0 ? -149 : e - 150;
+}
+
+template <typename T>
+__device__ T block_sum(T v, T *sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  T r = 0;
+  for (int w = 0; w < NORM_THREADS / 64; ++w) r += sh[w];
+  return r;
+}
+
+__device__ int block_min(int v, int *sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_min_i(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  int r = sh[0];
+  for (int w = 1; w < NORM_THREADS / 64; ++w) r = min(r, sh[w]);
+  return r;
+}
+
+__global__ void __launch_bounds__(NORM_THREADS) k_norm_exact(const float *__restrict__ X, float *__restrict__ Y, int n,
+                                                              const float *__restrict__ gw,
+                                                              const float *__restrict__ gb, unsigned *stats) {
+  extern __shared__ __attribute__((aligned(16))) float xrow[];
+  __shared__ double shd[NORM_THREADS / 64];
+  __shared__ int shi[NORM_THREADS / 64];
+  __shared__ double bcast_d;
+  __shared__ float bcast_f;
+  const float *x = X + (size_t)blockIdx.x * n;
+  float *y = Y + (size_t)blockIdx.x * n;
+  const double eps = 1e-5f;
+
+  double s = 0.0, sa = 0.0;
+  int um = 1 << 30;
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
+    const float v = x[i];
+    xrow[i] = v;
+    s += (double)v;
+    sa += (double)fabsf(v);
+    um = min(um, ulp_exp(v));
+  }
+  s = block_sum(s, shd);
+  sa = block_sum(sa, shd);
+  um = block_min(um, shi);
+  const bool exact = (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
+  if (!exact) {
+    if (threadIdx.x == 0) {
+      double m = 0.0;
+      for (int i = 0; i < n; ++i) m += xrow[i];
+      bcast_d = m;
+      if (stats) atomicAdd(&stats[0], 1u);
+    }
+    __syncthreads();
+    s = bcast_d;
+  }
+  const double mean = s / n;
+
+  double s2 = 0.0;
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
+    const double v = (double)xrow[i] - mean;
+    s2 += v * v;
+  }
+  s2 = block_sum(s2, shd);
+  const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
+  const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
+  const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
+  float scale = sc_lo;
+  if (sc_lo != sc_hi) {
+    if (threadIdx.x == 0) {
+      double q = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double v = (double)xrow[i] - mean;
+        q += v * v;
+      }
+      bcast_f = (float)(1.0 / sqrt(q / n + eps));
+      if (stats) atomicAdd(&stats[1], 1u);
+    }
+    __syncthreads();
+    scale = bcast_f;
+  }
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
+    float v = (float)((double)xrow[i] - mean);
+    v = v * scale;
+    if (gw) v = (gw[i] * v) + gb[i];  // ggml_add(ggml_mul(repeat(w), cur), repeat(b))
+    y[i] = v;
+  }
+}
+
+static unsigned *g_norm_stats = nullptr;  // device counters, see vsim_norm_stats
+
+int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s) {
+  if (k <= 0 || rows <= 0) { set_error("norm: bad shape"); return VSIM_EINVAL; }
+  if ((w == nullptr) != (b == nullptr)) { set_error("norm: affine needs both w and b"); return VSIM_EINVAL; }
+  if ((size_t)k * 4 > 64 * 1024) { set_error("norm: row longer than 16384"); return VSIM_EINVAL; }
+  hipLaunchKernelGGL(k_norm_exact, dim3(rows), dim3(NORM_THREADS), (size_t)k * 4, s, x, y, k, w, b, g_norm_stats);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ GELU via fp16 LUT
+// y = fp16->fp32(table_gelu_f16[fp32->fp16(x + bias)])  (bias add fused: ggml_add then
+// ggml_gelu, vsim.cpp:680-683)
+__global__ void k_gelu(const float *__restrict__ x, float *__restrict__ y, int n, const float *__restrict__ bias,
+                       int bias_len, const uint16_t *__restrict__ tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = x[i];
+  if (bias) v = v + bias[i % bias_len];
+  y[i] = h2f(tab[f2h(v)]);
+}
+
+int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s) {
+  DevTables t;
+  if (int rc = tables_get(&t)) return rc;
+  hipLaunchKernelGGL(k_gelu, dim3((n + 255) / 256), dim3(256), 0, s, x, y, n, bias, bias_len, t.gelu_f16);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ adds
+// GPT-NeoX parallel residual (vsim.cpp:694-695): inpL = inpL + (attn + ff)
+// non-parallel (vsim.cpp:631-657): inpL = ff + inpL — the reference adds only the FF
+// output back (the attention output reaches inpL only through the FF LayerNorm input).
+__global__ void k_add_residual(float *__restrict__ inpL, const float *__restrict__ attn, const float *__restrict__ ff,
+                               int n, int serial) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  inpL[i] = serial ? ff[i] + inpL[i] : inpL[i] + (attn[i] + ff[i]);
+}
+
+int launch_add_residual(float *inpL, const float *attn, const float *ff, int n, int serial, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_residual, dim3((n + 255) / 256), dim3(256), 0, s, inpL, attn, ff, n, serial);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+__global__ void k_add_bias(float *x, const float *b, int k, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k * n) return;
+  x[i] = x[i] + b[i % k];
+}
+
+int launch_add_bias(float *x, const float *b, int k, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_bias, dim3((k * n + 255) / 256), dim3(256), 0, s, x, b, k, n);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ fp16 tables
+// Host-built exactly as ggml_init does (ggml.c:1240-1251: glibc exp/tanh in double,
+// then fp32 -> fp16 by the bit-exact converter), uploaded once per device.
+static float host_h2f(uint16_t h) {
+  const uint32_t w = (uint32_t)h << 16;
+  const uint32_t sign = w & 0x80000000u;
+  const uint32_t two_w = w + w;
+  uint32_t a = (two_w >> 4) + (0xE0u << 23), b = (two_w >> 17) | (126u << 23);
+  float fa, fb;
+  memcpy(&fa, &a, 4);
+  memcpy(&fb, &b, 4);
+  const float normalized = fa * 0x1.0p-112f;
+  const float denormalized = fb - 0.5f;
+  uint32_t rn, rd;
+  memcpy(&rn, &normalized, 4);
+  memcpy(&rd, &denormalized, 4);
+  const uint32_t r = sign | (two_w < (1u << 27) ? rd : rn);
+  float f;
+  memcpy(&f, &r, 4);
+  return f;
+}
+
+static uint16_t host_f2h(float f) {
+  volatile float base = (fabsf(f) * 0x1.0p+112f);
+  base = base * 0x1.0p-110f;
+  uint32_t w;
+  memcpy(&w, &f, 4);
+  const uint32_t shl1_w = w + w;
+  const uint32_t sign = w & 0x80000000u;
+  uint32_t bias = shl1_w & 0xFF000000u;
+  if (bias < 0x71000000u) bias = 0x71000000u;
+  const uint32_t bb = (bias >> 1) + 0x07800000u;
+  float fb;
+  memcpy(&fb, &bb, 4);
+  const float sum = fb + base;
+  uint32_t bits;
+  memcpy(&bits, &sum, 4);
+  const uint32_t exp_bits = (bits >> 13) & 0x00007C00u;
+  const uint32_t mantissa_bits = bits & 0x00000FFFu;
+  const uint32_t nonsign = exp_bits + mantissa_bits;
+  return (uint16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+
+static float host_gelu(float x) {
+  const double A = 0.044715, S = 0.79788456;
+  return 0.5 * x * (1.0 + tanh(S * x * (1.0 + A * x * x)));
+}
+
+static std::mutex g_tab_mu;
+static std::vector<uint16_t> g_exp_host, g_gelu_host;
+static DevTables g_dev_tab[64];
+static bool g_dev_tab_ok[64];
+
+static void build_host_tables() {
+  if (!g_exp_host.empty()) return;
+  g_exp_host.resize(65536);
+  g_gelu_host.resize(65536);
+  for (int i = 0; i < 65536; ++i) {
+    const float f = host_h2f((uint16_t)i);
+    g_gelu_host[i] = host_f2h(host_gelu(f));
+    g_exp_host[i] = host_f2h((float)exp((double)f));
+  }
+}
+
+int tables_get(DevTables *t) {
+  int dev = 0;
+  VSIM_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  if (dev < 0 || dev >= 64) { set_error("tables: device id out of range"); return VSIM_EINVAL; }
+  if (!g_dev_tab_ok[dev]) {
+    build_host_tables();
+    uint16_t *p = nullptr;
+    VSIM_HIP(hipMalloc(&p, 2 * 65536 * sizeof(uint16_t)));
+    VSIM_HIP(hipMemcpy(p, g_exp_host.data(), 65536 * 2, hipMemcpyHostToDevice));
+    VSIM_HIP(hipMemcpy(p + 65536, g_gelu_host.data(), 65536 * 2, hipMemcpyHostToDevice));
+    g_dev_tab[dev].exp_f16 = p;
+    g_dev_tab[dev].gelu_f16 = p + 65536;
+    g_dev_tab_ok[dev] = true;
+    if (!g_norm_stats) {
+      VSIM_HIP(hipMalloc(&g_norm_stats, 4 * sizeof(unsigned)));
+      VSIM_HIP(hipMemset(g_norm_stats, 0, 4 * sizeof(unsigned)));
+    }
+  }
+  *t = g_dev_tab[dev];
+  return VSIM_OK;
+}
+
+int tables_host(uint16_t *exp_f16, uint16_t *gelu_f16) {
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  build_host_tables();
+  memcpy(exp_f16, g_exp_host.data(), 65536 * 2);
+  memcpy(gelu_f16, g_gelu_host.data(), 65536 * 2);
+  return VSIM_OK;
+}
+
+int norm_stats(unsigned *out2) {
+  if (!g_norm_stats) { out2[0] = out2[1] = 0; return VSIM_OK; }
+  unsigned h[4];
+  VSIM_HIP(hipMemcpy(h, g_norm_stats, sizeof(h), hipMemcpyDeviceToHost));
+  out2[0] = h[0];
+  out2[1] = h[1];
+  return VSIM_OK;
+}
+
+}  // namespace vsim

@@ -1,0 +1,195 @@
+"""ctypes binding of libvsim_hip.so (include/vsim_hip.h).
+
+The HIP library is the product; this module only marshals arguments.  There is no
+CPU fallback: if the library is missing or a call fails, an exception is raised.
+Device buffers are torch tensors on a ROCm device (torch is plumbing here: memory and
+streams), passed to the C-ABI as raw pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libvsim_hip.so")
+
+MODE_EXACT = 0
+MODE_FAST = 1
+ARCH_GPTNEOX = 0
+ARCH_GPTJ = 1
+
+# symbols declared in include/vsim_hip.h (checked by tests/test_capi.py)
+EXPORTS = [
+    "vsim_last_error", "vsim_device_count", "vsim_q4_bytes",
+    "init_xmax", "imax_ggml_compute_forward_mul_mat_q4_0_f32",
+    "vsim_ggml_gptneox_rope_f32", "vsim_ggml_rope_f32", "vsim_ggml_soft_max_f32", "vsim_ggml_mul_mat_f32",
+    "vsim_dropin_stats", "vsim_dropin_reset",
+    "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_get_rows",
+    "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
+    "vsim_op_tables",
+    "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_randomize",
+    "vsim_model_set_mode", "vsim_model_hparams", "vsim_model_eval", "vsim_model_stream",
+    "vsim_model_logits_dev", "vsim_model_info", "vsim_model_set_graph", "vsim_model_set_profile",
+    "vsim_model_profile_stats", "vsim_model_free",
+]
+
+_lib = None
+
+
+class VsimError(RuntimeError):
+    pass
+
+
+class HParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("n_vocab", "n_embd", "n_head", "n_layer", "n_rot", "use_parallel_residual")]
+
+
+def lib():
+    """Load libvsim_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VsimError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, ci, cf, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    L.vsim_last_error.restype = ctypes.c_char_p
+    L.vsim_q4_bytes.restype = sz
+    L.vsim_q4_bytes.argtypes = [ci, ci]
+    L.vsim_op_q4_repack.argtypes = [vp, vp, ci, ci, vp]
+    L.vsim_op_q4_unpack.argtypes = [vp, vp, ci, ci, vp]
+    L.vsim_op_q4_quantize.argtypes = [vp, ci, ci, vp, vp, vp]
+    L.vsim_op_q4_gemv.argtypes = [vp, ci, ci, vp, vp, ci, vp, vp, ci, vp]
+    L.vsim_op_get_rows.argtypes = [vp, ci, ci, vp, ci, vp, vp]
+    L.vsim_op_norm.argtypes = [vp, vp, ci, ci, vp, vp, vp]
+    L.vsim_op_gelu.argtypes = [vp, vp, ci, vp]
+    L.vsim_op_attn_softmax.argtypes = [vp, ci, ci, ci, ci, cf, vp]
+    L.vsim_op_rope.argtypes = [ci, vp, ci, ci, ci, ci, ci, ci, vp]
+    L.vsim_op_kq.argtypes = [vp, ci, vp, ci, ci, ci, ci, ci, vp, vp]
+    L.vsim_op_kqv.argtypes = [vp, ci, vp, ci, ci, ci, ci, vp, vp]
+    L.vsim_op_tables.argtypes = [vp, vp]
+    L.vsim_model_create.argtypes = [ci, ctypes.POINTER(HParams), ci, ci, ci, ci, ctypes.POINTER(vp)]
+    L.vsim_model_load_file.argtypes = [ctypes.c_char_p, ci, ci, ci, ci, ci, ctypes.POINTER(vp)]
+    L.vsim_model_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, sz]
+    L.vsim_model_randomize.argtypes = [vp, ctypes.c_uint64, cf]
+    L.vsim_model_set_mode.argtypes = [vp, ci]
+    L.vsim_model_set_graph.argtypes = [vp, ci]
+    L.vsim_model_hparams.argtypes = [vp, ctypes.POINTER(HParams), ctypes.POINTER(ci), ctypes.POINTER(ci),
+                                     ctypes.POINTER(ci)]
+    L.vsim_model_eval.argtypes = [vp, ci, vp, ci, vp, vp, vp]
+    L.vsim_model_stream.restype = vp
+    L.vsim_model_stream.argtypes = [vp]
+    L.vsim_model_logits_dev.restype = vp
+    L.vsim_model_logits_dev.argtypes = [vp]
+    L.vsim_model_info.argtypes = [vp, ctypes.POINTER(ci), ctypes.POINTER(ci), ctypes.POINTER(sz)]
+    L.vsim_model_free.argtypes = [vp]
+    L.vsim_model_set_profile.argtypes = [vp, ci]
+    L.vsim_model_profile_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long),
+                                           ctypes.POINTER(ctypes.c_double)]
+    L.vsim_dropin_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().vsim_last_error().decode(errors="replace")
+        raise VsimError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Raw pointer of a torch tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def q4_bytes(rows: int, k: int) -> int:
+    return int(lib().vsim_q4_bytes(rows, k))
+
+
+class Model:
+    """Device-resident model executor (vsim_model_* in include/vsim_hip.h)."""
+
+    def __init__(self, handle, arch):
+        self.h = handle
+        self.arch = arch
+        hp = HParams()
+        n_ctx, lb, le = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().vsim_model_hparams(self.h, ctypes.byref(hp), ctypes.byref(n_ctx), ctypes.byref(lb),
+                                       ctypes.byref(le)), "hparams")
+        self.hp = hp
+        self.n_ctx = n_ctx.value
+        self.layer_begin, self.layer_end = lb.value, le.value
+        self.n_vocab, self.n_embd = hp.n_vocab, hp.n_embd
+        self.first = self.layer_begin == 0
+        self.last = self.layer_end == hp.n_layer
+
+    @classmethod
+    def load(cls, path, arch, n_ctx=512, device=0, layer_begin=0, layer_end=-1):
+        h = ctypes.c_void_p()
+        check(lib().vsim_model_load_file(path.encode(), arch, n_ctx, device, layer_begin, layer_end,
+                                         ctypes.byref(h)), f"load {path}")
+        return cls(h, arch)
+
+    @classmethod
+    def create(cls, arch, hp: dict, n_ctx=512, device=0, layer_begin=0, layer_end=-1):
+        h = ctypes.c_void_p()
+        c = HParams(**hp)
+        check(lib().vsim_model_create(arch, ctypes.byref(c), n_ctx, device, layer_begin, layer_end,
+                                      ctypes.byref(h)), "create")
+        return cls(h, arch)
+
+    def randomize(self, seed=0, std=0.02):
+        check(lib().vsim_model_randomize(self.h, seed, std), "randomize")
+
+    def set_mode(self, mode):
+        check(lib().vsim_model_set_mode(self.h, mode), "set_mode")
+
+    def set_graph(self, enable: bool):
+        check(lib().vsim_model_set_graph(self.h, 1 if enable else 0), "set_graph")
+
+    def eval(self, n_past, tokens=None, resid_in=None, resid_out=None, want_logits=True):
+        N = len(tokens) if tokens is not None else int(resid_in.shape[0])
+        tok = np.ascontiguousarray(tokens, np.int32) if tokens is not None else None
+        lg = np.zeros(self.n_vocab, np.float32) if (want_logits and self.last) else None
+        check(lib().vsim_model_eval(self.h, n_past, ptr(tok), N, ptr(resid_in), ptr(resid_out), ptr(lg)), "eval")
+        return lg
+
+    def info(self):
+        k, g, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
+        check(lib().vsim_model_info(self.h, ctypes.byref(k), ctypes.byref(g), ctypes.byref(w)), "info")
+        return {"kernels_per_eval": k.value, "graph": bool(g.value), "weight_bytes": w.value}
+
+    def set_profile(self, enable: bool):
+        check(lib().vsim_model_set_profile(self.h, 1 if enable else 0), "set_profile")
+
+    def profile_stats(self):
+        ms, n, b = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
+        check(lib().vsim_model_profile_stats(self.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "prof")
+        return {"gemv_ms": ms.value, "gemv_launches": n.value, "gemv_bytes": b.value}
+
+    def stream(self) -> int:
+        return lib().vsim_model_stream(self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().vsim_model_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def dropin_stats():
+    v = [ctypes.c_uint64() for _ in range(4)]
+    lib().vsim_dropin_stats(*[ctypes.byref(x) for x in v])
+    return {"calls": v[0].value, "h2d": v[1].value, "d2h": v[2].value, "cached": v[3].value}
