@@ -16,10 +16,14 @@
  *     and GPT-J graphs, whole decode step captured in a hipGraph; host<->device traffic
  *     per token is the token ids in and one logits row out (vsim.cpp:736-737).
  *
- * Device weight layout ("Q4 SoA"): a Q4_0 matrix of M rows x K weights keeps the
+ * Device weight layout ("W4T32"): a Q4_0 matrix of M rows x K weights keeps the
  * reference's 0.625 B/weight but splits the 20-byte blocks (ggml.c:204-251) into a
- * 16-byte-aligned nibble plane qs[M][K/32][16] followed by the scale plane d[M][K/32]
- * (fp32).  vsim_q4_bytes(M, K) == M*K/32*20 bytes.
+ * 16-byte nibble plane followed by an fp32 scale plane, with rows grouped in tiles of 32
+ * and, inside a tile, block b of all 32 rows stored contiguously (512 B of nibbles,
+ * 128 B of scales) so row-per-lane waves read whole cache lines.  M is padded to a
+ * multiple of 32: vsim_q4_bytes(M, K) = ceil(M/32)*32 * K/32 * 20 bytes.
+ * Activation rows (vsim_op_q4_quantize output, "Q4 SoA"): nibble plane [n][K/32][16] then
+ * scale plane [n][K/32], n*K/32*20 bytes.
  *
  * Every function returns 0 on success or a negative VSIM_E* code; vsim_last_error()
  * describes the last failure of the calling thread.
@@ -76,8 +80,12 @@ void vsim_dropin_reset(void);
 
 /* ------------------------------------------------------- 2. op-level (device ptrs) -- */
 /* `stream` is a hipStream_t passed as void* (NULL = default stream). */
-int vsim_op_q4_repack(const void *aos, void *soa, int rows, int k, void *stream);
-int vsim_op_q4_unpack(const void *soa, void *aos, int rows, int k, void *stream);
+/* weights: ggml AoS blocks <-> W4T32 */
+int vsim_op_q4_repack(const void *aos, void *w, int rows, int k, void *stream);
+int vsim_op_q4_unpack(const void *w, void *aos, int rows, int k, void *stream);
+/* activation rows: ggml AoS blocks <-> Q4 SoA */
+int vsim_op_act_repack(const void *aos, void *xq, int n, int k, void *stream);
+int vsim_op_act_unpack(const void *xq, void *aos, int n, int k, void *stream);
 /* quantize_row_q4_0 (ggml.c:209-251) of n rows of k floats: xq in Q4 SoA, xd = the
  * dequantized values d*(q-8) the exact GEMV multiplies with (ggml.c:497-498). */
 int vsim_op_q4_quantize(const float *x, int k, int n, void *xq, float *xd, void *stream);

@@ -57,17 +57,23 @@ def test_repack_roundtrip():
     rng = np.random.default_rng(0)
     aos = mg.quantize_q4_0(rng.standard_normal(96 * 256).astype(np.float32))
     soa = repack(aos, 96, 256)
-    back = torch.empty_like(soa)
+    back = torch.empty(aos.size, dtype=torch.uint8, device=DEV)
     hip.check(hip.lib().vsim_op_q4_unpack(soa.data_ptr(), back.data_ptr(), 96, 256, None), "unpack")
     assert np.array_equal(host(back), aos)
+    # rows not a multiple of the 32-row tile (pythia's 50288-row head)
+    aos2 = mg.quantize_q4_0(rng.standard_normal(50 * 64).astype(np.float32))
+    w2 = repack(aos2, 50, 64)
+    back2 = torch.empty(aos2.size, dtype=torch.uint8, device=DEV)
+    hip.check(hip.lib().vsim_op_q4_unpack(w2.data_ptr(), back2.data_ptr(), 50, 64, None), "unpack")
+    assert np.array_equal(host(back2), aos2)
 
 
 def test_quantize_bit_exact():
     z = ops("qrow")
     x = z["x"]
     xq, _ = quantize(x, x.size, 1)
-    aos = torch.empty_like(xq)
-    hip.check(hip.lib().vsim_op_q4_unpack(xq.data_ptr(), aos.data_ptr(), 1, x.size, None), "unpack")
+    aos = torch.empty(x.size // 32 * 20, dtype=torch.uint8, device=DEV)
+    hip.check(hip.lib().vsim_op_act_unpack(xq.data_ptr(), aos.data_ptr(), 1, x.size, None), "unpack")
     assert np.array_equal(host(aos), z["y"])
 
 
@@ -92,8 +98,8 @@ def test_gemv_fast_within_bound(c):
     w = repack(c["w"], M, K)
     xq, xd = quantize(c["x"], K, N)
     y = gemv(w, M, K, xq, xd, N, hip.MODE_FAST).reshape(N, M)
-    xq_aos = torch.empty_like(xq)
-    hip.check(hip.lib().vsim_op_q4_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
+    xq_aos = torch.empty(N * K // 32 * 20, dtype=torch.uint8, device=DEV)
+    hip.check(hip.lib().vsim_op_act_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
     exact, absum = _fp64_product(c["w"], M, K, host(xq_aos), N)
     # tolerance: |y - y64| <= 4*K*2^-24 * sum|w_i x_i| (fp32 accumulation bound, well above
     # the observed error); the reference's own chain meets the same bound

@@ -16,7 +16,6 @@
 
 namespace vsim {
 int tables_host(uint16_t *exp_f16, uint16_t *gelu_f16);
-int launch_q4_dequant(const void *soa, int rows, int k, float *y, hipStream_t s);
 }  // namespace vsim
 
 using namespace vsim;
@@ -35,6 +34,12 @@ int vsim_op_q4_repack(const void *aos, void *soa, int rows, int k, void *stream)
 }
 int vsim_op_q4_unpack(const void *soa, void *aos, int rows, int k, void *stream) {
   return launch_q4_unpack(soa, aos, rows, k, (hipStream_t)stream);
+}
+int vsim_op_act_repack(const void *aos, void *xq, int n, int k, void *stream) {
+  return launch_act_repack(aos, xq, n, k, (hipStream_t)stream);
+}
+int vsim_op_act_unpack(const void *xq, void *aos, int n, int k, void *stream) {
+  return launch_act_unpack(xq, aos, n, k, (hipStream_t)stream);
 }
 int vsim_op_q4_quantize(const float *x, int k, int n, void *xq, float *xd, void *stream) {
   return launch_q4_quantize(x, k, n, xq, xd, (hipStream_t)stream);
@@ -193,7 +198,7 @@ void imax_ggml_compute_forward_mul_mat_q4_0_f32(int THREAD, int LANE, const stru
   if (it == g.wcache.end() || it->second.rows != M || it->second.k != K) {
     const size_t wb = (size_t)M * K / QK * QBYTES;
     void *dev = nullptr, *stage = nullptr;
-    if (hipMalloc(&dev, wb) != hipSuccess || hipMalloc(&stage, wb) != hipSuccess) die("weight cache alloc");
+    if (hipMalloc(&dev, w4_bytes(M, K)) != hipSuccess || hipMalloc(&stage, wb) != hipSuccess) die("weight cache alloc");
     if (hipMemcpyAsync(stage, src0->data, wb, hipMemcpyHostToDevice, s) != hipSuccess) die("weight upload");
     if (launch_q4_repack(stage, dev, M, K, s)) die("weight repack");
     if (hipStreamSynchronize(s) != hipSuccess) die("weight upload sync");
@@ -209,7 +214,7 @@ void imax_ggml_compute_forward_mul_mat_q4_0_f32(int THREAD, int LANE, const stru
       grow((void **)&g.xd, &g.xd_cap, (size_t)N * K * 4) || grow((void **)&g.y, &g.y_cap, (size_t)N * M * 4))
     die("activation alloc");
   if (hipMemcpyAsync(g.act_aos, params->wdata, ab, hipMemcpyHostToDevice, s) != hipSuccess) die("activation upload");
-  if (launch_q4_repack(g.act_aos, g.act_soa, N, K, s)) die("activation repack");
+  if (launch_act_repack(g.act_aos, g.act_soa, N, K, s)) die("activation repack");
   if (launch_q4_dequant(g.act_soa, N, K, g.xd, s)) die("activation dequant");
   if (launch_q4_gemv(it->second.dev, M, K, g.act_soa, g.xd, N, nullptr, g.y, g.mode, s)) die("gemv");
   if (hipMemcpyAsync(dst->data, g.y, (size_t)N * M * 4, hipMemcpyDeviceToHost, s) != hipSuccess) die("result copy");

@@ -16,25 +16,50 @@ namespace vsim {
 constexpr int QK = 32;       // weights per Q4_0 block (ggml.c:204)
 constexpr int QBYTES = 20;   // fp32 d + 16 nibble bytes (ggml.c:907-909)
 
-// ---------------------------------------------------------------- Q4 SoA views
-// Device layout of a Q4_0 matrix: nibble plane qs[rows][nb][16], then scale plane
-// d[rows][nb] (fp32).  Same 0.625 B/weight as the ggml AoS block.
-struct Q4View {
+// ---------------------------------------------------------------- weight layout W4T32
+// Q4_0 weight matrix of `rows` x `k`: rows padded to tiles of T32; inside a tile block b
+// of its 32 rows is contiguous.  Nibble plane qs (16 B per block) first, then the fp32
+// scale plane d: block (r, b) lives at index ((r/32)*nb + b)*32 + r%32 of both.
+constexpr int T32 = 32;
+
+struct W4 {
   const uint8_t *qs;
   const float *d;
-  int rows, k;
+  int rows, k, tiles;
   __host__ __device__ int nb() const { return k / QK; }
+  __host__ __device__ size_t off(int r, int b) const {
+    return ((size_t)(r / T32) * nb() + b) * T32 + (r & (T32 - 1));
+  }
 };
 
-inline Q4View q4_view(const void *base, int rows, int k) {
-  const size_t nb = (size_t)k / QK;
-  Q4View v;
-  v.qs = (const uint8_t *)base;
-  v.d = (const float *)((const uint8_t *)base + (size_t)rows * nb * 16);
+inline size_t w4_bytes(int rows, int k) { return (size_t)((rows + T32 - 1) / T32) * T32 * (k / QK) * QBYTES; }
+
+inline W4 w4_view(const void *base, int rows, int k) {
+  W4 v;
   v.rows = rows;
   v.k = k;
+  v.tiles = (rows + T32 - 1) / T32;
+  const size_t nblk = (size_t)v.tiles * T32 * (k / QK);
+  v.qs = (const uint8_t *)base;
+  v.d = (const float *)((const uint8_t *)base + nblk * 16);
   return v;
 }
+
+// A batch of up to 4 independent GEMVs (same token) in one launch; workgroups take the
+// tiles of job 0, then job 1, ...  Activation operands: xd = dequantized factors (exact
+// mode), xqs/xdd = Q4_0 nibbles and scales of the activation row (fast mode).
+struct GemvJob {
+  W4 w;
+  const float *xd;
+  const uint8_t *xqs;
+  const float *xdd;
+  const float *bias;
+  float *y;
+};
+struct GemvBatch {
+  GemvJob j[4];
+  int nj;
+};
 
 // ---------------------------------------------------------------- fp16 (ggml.c:95-142)
 __device__ __forceinline__ float bits_f(uint32_t w) { return __uint_as_float(w); }
@@ -62,6 +87,16 @@ __device__ __forceinline__ uint16_t f2h(float f) {
   const uint32_t mantissa_bits = bits & 0x00000FFFu;
   const uint32_t nonsign = exp_bits + mantissa_bits;
   return (uint16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+
+// (int8_t)round(v) as the reference's x86 build evaluates it (ggml.c:239-240): round to
+// nearest, ties away from zero, then cvttsd2si — whose out-of-range / NaN result is
+// INT_MIN (low byte 0) where the GPU's v_cvt_i32_f32 would saturate.  Matters only for
+// the degenerate blocks whose id = 1/d overflows (subnormal amax).
+__device__ __forceinline__ int x86_round_i8(float v) {
+  const float r = roundf(v);
+  const int i = fabsf(r) < 2147483648.0f ? (int)r : (int)0x80000000u;
+  return (int)(int8_t)i;
 }
 
 // ---------------------------------------------------------------- wave reductions
@@ -108,6 +143,10 @@ int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s)
 int launch_q4_quantize(const float *x, int k, int n, void *xq, float *xd, hipStream_t s);
 int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias,
                    float *y, int mode, hipStream_t s);
+int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s);
+int launch_act_repack(const void *aos, void *xq, int n, int k, hipStream_t s);
+int launch_act_unpack(const void *xq, void *aos, int n, int k, hipStream_t s);
+int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s);
 int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s);
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);

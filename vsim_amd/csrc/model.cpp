@@ -188,9 +188,11 @@ void plan_slots(vsim_model *m, std::vector<std::pair<std::string, Slot>> &out) {
   }
 }
 
+// bytes of the tensor in the ggml file (AoS blocks) and on the device (W4T32, padded)
 size_t slot_bytes(const Slot &s) {
   return s.kind == KQ4 ? (size_t)s.rows * s.k / QK * QBYTES : (size_t)s.k * sizeof(float);
 }
+size_t slot_dev_bytes(const Slot &s) { return s.kind == KQ4 ? w4_bytes(s.rows, s.k) : (size_t)s.k * sizeof(float); }
 
 void bind_pointers(vsim_model *m) {
   auto P = [&](const std::string &n) -> void * {
@@ -352,7 +354,7 @@ int vsim_device_count(void) {
   return n;
 }
 
-size_t vsim_q4_bytes(int rows, int k) { return (size_t)rows * k / QK * QBYTES; }
+size_t vsim_q4_bytes(int rows, int k) { return w4_bytes(rows, k); }
 
 int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
                       vsim_model **out) {
@@ -385,13 +387,13 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   std::vector<std::pair<std::string, Slot>> plan;
   plan_slots(m, plan);
   size_t tot = 0;
-  for (auto &ps : plan) tot += (slot_bytes(ps.second) + 255) & ~(size_t)255;
+  for (auto &ps : plan) tot += (slot_dev_bytes(ps.second) + 255) & ~(size_t)255;
   if (hipMalloc((void **)&m->warena, tot) != hipSuccess) { set_error("model_create: weight alloc failed"); return fail(VSIM_ENOMEM); }
   m->wbytes = tot;
   size_t off = 0;
   for (auto &ps : plan) {
     ps.second.ptr = m->warena + off;
-    off += (slot_bytes(ps.second) + 255) & ~(size_t)255;
+    off += (slot_dev_bytes(ps.second) + 255) & ~(size_t)255;
     m->slots[ps.first] = ps.second;
   }
   bind_pointers(m);

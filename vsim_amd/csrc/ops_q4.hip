@@ -1,29 +1,81 @@
-// vsim_amd/csrc/ops_q4.hip — Q4_0 kernels for gfx950: layout repack, activation
+// vsim_amd/csrc/ops_q4.hip — Q4_0 kernels for gfx950: weight tiling, activation
 // quantization, the decode GEMV (exact and fast), embedding get_rows.
 //
 // Reference behaviour restated (not translated):
 //   quantize_row_q4_0        ggml.c:209-251
 //   dequantize_row_q4_0      ggml.c:301-334 (get_rows, ggml.c:5603-5628)
 //   Q4_0 x Q4_0 dot          imax.c:1182-1230 (== ggml_vec_dot_q4_0, ggml.c:472-511)
+//
+// Weight layout "W4T32" (see W4 in common.hpp): rows are grouped in tiles of 32; inside a
+// tile the 16-byte nibble blocks are stored block-major, so the 32 rows' block b sit in
+// 512 contiguous bytes and the 32 scales of block b in 128 contiguous bytes.  A wave whose
+// lanes own rows reads whole cache lines; bytes per weight stay 0.625.
 #include "common.hpp"
 #include "../../include/vsim_hip.h"
 
 namespace vsim {
 
-// ------------------------------------------------------------------ repack AoS <-> SoA
-__global__ void k_q4_aos2soa(const uint8_t *__restrict__ aos, uint8_t *__restrict__ qs, float *__restrict__ d,
-                             size_t nblocks) {
-  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  const uint32_t *src = (const uint32_t *)(aos + b * QBYTES);  // blocks are 4-byte aligned
-  d[b] = __uint_as_float(src[0]);
-  uint4 q;
-  q.x = src[1]; q.y = src[2]; q.z = src[3]; q.w = src[4];
-  *(uint4 *)(qs + b * 16) = q;
+// ------------------------------------------------------------------ W4T32 pack / unpack
+__global__ void k_w4_pack(const uint8_t *__restrict__ aos, W4 W) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = W.nb();
+  const size_t total = (size_t)W.tiles * T32 * nb;
+  if (i >= total) return;
+  // i enumerates (row, block) in row-major order over the padded rows
+  const int r = (int)(i / nb), b = (int)(i % nb);
+  const size_t o = W.off(r, b);
+  if (r >= W.rows) {  // padding rows of the last tile: d = 0, q = 8 (value 0)
+    ((float *)W.d)[o] = 0.0f;
+    *(uint4 *)(W.qs + o * 16) = make_uint4(0x88888888u, 0x88888888u, 0x88888888u, 0x88888888u);
+    return;
+  }
+  const uint32_t *src = (const uint32_t *)(aos + i * QBYTES);  // AoS blocks are 4-byte aligned
+  ((float *)W.d)[o] = __uint_as_float(src[0]);
+  *(uint4 *)(W.qs + o * 16) = make_uint4(src[1], src[2], src[3], src[4]);
 }
 
-__global__ void k_q4_soa2aos(const uint8_t *__restrict__ qs, const float *__restrict__ d, uint8_t *__restrict__ aos,
-                             size_t nblocks) {
+__global__ void k_w4_unpack(W4 W, uint8_t *__restrict__ aos) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = W.nb();
+  if (i >= (size_t)W.rows * nb) return;
+  const int r = (int)(i / nb), b = (int)(i % nb);
+  const size_t o = W.off(r, b);
+  uint32_t *dst = (uint32_t *)(aos + i * QBYTES);
+  const uint4 q = *(const uint4 *)(W.qs + o * 16);
+  dst[0] = __float_as_uint(W.d[o]);
+  dst[1] = q.x; dst[2] = q.y; dst[3] = q.z; dst[4] = q.w;
+}
+
+int launch_q4_repack(const void *aos, void *w, int rows, int k, hipStream_t s) {
+  if (k % QK || rows <= 0) { set_error("q4_repack: k must be a multiple of 32"); return VSIM_EINVAL; }
+  const W4 W = w4_view(w, rows, k);
+  const size_t tot = (size_t)W.tiles * T32 * W.nb();
+  hipLaunchKernelGGL(k_w4_pack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, (const uint8_t *)aos, W);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+int launch_q4_unpack(const void *w, void *aos, int rows, int k, hipStream_t s) {
+  if (k % QK || rows <= 0) { set_error("q4_unpack: k must be a multiple of 32"); return VSIM_EINVAL; }
+  const W4 W = w4_view(w, rows, k);
+  const size_t tot = (size_t)rows * W.nb();
+  hipLaunchKernelGGL(k_w4_unpack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, W, (uint8_t *)aos);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// activation rows (AoS, as the reference's INIT phase writes them) -> row-major SoA
+__global__ void k_act_aos2soa(const uint8_t *__restrict__ aos, uint8_t *__restrict__ qs, float *__restrict__ d,
+                              size_t nblocks) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const uint32_t *src = (const uint32_t *)(aos + b * QBYTES);
+  d[b] = __uint_as_float(src[0]);
+  *(uint4 *)(qs + b * 16) = make_uint4(src[1], src[2], src[3], src[4]);
+}
+
+__global__ void k_act_soa2aos(const uint8_t *__restrict__ qs, const float *__restrict__ d, uint8_t *__restrict__ aos,
+                              size_t nblocks) {
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nblocks) return;
   uint32_t *dst = (uint32_t *)(aos + b * QBYTES);
@@ -32,23 +84,22 @@ __global__ void k_q4_soa2aos(const uint8_t *__restrict__ qs, const float *__rest
   dst[1] = q.x; dst[2] = q.y; dst[3] = q.z; dst[4] = q.w;
 }
 
-int launch_q4_repack(const void *aos, void *soa, int rows, int k, hipStream_t s) {
-  if (k % QK || rows <= 0) { set_error("q4_repack: k must be a multiple of 32"); return VSIM_EINVAL; }
-  const size_t nbk = (size_t)rows * (k / QK);
-  uint8_t *qs = (uint8_t *)soa;
+int launch_act_repack(const void *aos, void *xq, int n, int k, hipStream_t s) {
+  const size_t nbk = (size_t)n * (k / QK);
+  uint8_t *qs = (uint8_t *)xq;
   float *d = (float *)(qs + nbk * 16);
-  hipLaunchKernelGGL(k_q4_aos2soa, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, (const uint8_t *)aos, qs, d,
-                     nbk);
+  hipLaunchKernelGGL(k_act_aos2soa, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, (const uint8_t *)aos, qs,
+                     d, nbk);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
 
-int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s) {
-  if (k % QK || rows <= 0) { set_error("q4_unpack: k must be a multiple of 32"); return VSIM_EINVAL; }
-  const size_t nbk = (size_t)rows * (k / QK);
-  const uint8_t *qs = (const uint8_t *)soa;
+int launch_act_unpack(const void *xq, void *aos, int n, int k, hipStream_t s) {
+  const size_t nbk = (size_t)n * (k / QK);
+  const uint8_t *qs = (const uint8_t *)xq;
   const float *d = (const float *)(qs + nbk * 16);
-  hipLaunchKernelGGL(k_q4_soa2aos, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, qs, d, (uint8_t *)aos, nbk);
+  hipLaunchKernelGGL(k_act_soa2aos, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, qs, d, (uint8_t *)aos,
+                     nbk);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -58,6 +109,31 @@ int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s)
 // (correctly rounded division), id = 1/d, q = (int8)round(x*id) + 8 with round-half-
 // away-from-zero, nibble pairs (q[2l], q[2l+1]).  Also emits xd = d*(q-8) per element,
 // the activation factor f2/f3 of the reference dot (ggml.c:497-498).
+__device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, float *d_out, float *xd_out) {
+  float amax = 0.0f;
+#pragma unroll
+  for (int l = 0; l < QK; ++l) amax = amax > fabsf(v[l]) ? amax : fabsf(v[l]);
+  const float d = amax / 7.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  uint32_t w[4] = {0, 0, 0, 0};
+  float out[QK];
+#pragma unroll
+  for (int l = 0; l < QK; l += 2) {
+    const int q0 = x86_round_i8(v[l] * id) + 8;
+    const int q1 = x86_round_i8(v[l + 1] * id) + 8;
+    w[l / 8] |= (uint32_t)((q0 & 0xF) | ((q1 & 0xF) << 4)) << (8 * ((l / 2) & 3));
+    out[l] = d * (float)(q0 - 8);
+    out[l + 1] = d * (float)(q1 - 8);
+  }
+  *(uint4 *)qs_out = make_uint4(w[0], w[1], w[2], w[3]);
+  *d_out = d;
+  if (xd_out) {
+    float4 *o = (float4 *)xd_out;
+#pragma unroll
+    for (int i = 0; i < QK / 4; ++i) o[i] = make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
+  }
+}
+
 __global__ void k_q4_quantize(const float *__restrict__ x, int k, int n, uint8_t *__restrict__ qs,
                               float *__restrict__ dd, float *__restrict__ xd) {
   const int nb = k / QK;
@@ -70,28 +146,7 @@ __global__ void k_q4_quantize(const float *__restrict__ x, int k, int n, uint8_t
     const float4 t = src[i];
     v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
   }
-  float amax = 0.0f;
-#pragma unroll
-  for (int l = 0; l < QK; ++l) amax = amax > fabsf(v[l]) ? amax : fabsf(v[l]);
-  const float d = amax / 7.0f;
-  const float id = d != 0.0f ? 1.0f / d : 0.0f;
-  uint32_t w[4] = {0, 0, 0, 0};
-  float out[QK];
-#pragma unroll
-  for (int l = 0; l < QK; l += 2) {
-    const int q0 = (int)(int8_t)roundf(v[l] * id) + 8;
-    const int q1 = (int)(int8_t)roundf(v[l + 1] * id) + 8;
-    w[l / 8] |= (uint32_t)((q0 & 0xF) | ((q1 & 0xF) << 4)) << (8 * ((l / 2) & 3));
-    out[l] = d * (float)(q0 - 8);
-    out[l + 1] = d * (float)(q1 - 8);
-  }
-  *(uint4 *)(qs + (size_t)b * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-  dd[b] = d;
-  if (xd) {
-    float4 *o = (float4 *)(xd + (size_t)b * QK);
-#pragma unroll
-    for (int i = 0; i < QK / 4; ++i) o[i] = make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
-  }
+  quantize_block(v, qs + (size_t)b * 16, dd + b, xd ? xd + (size_t)b * QK : nullptr);
 }
 
 int launch_q4_quantize(const float *x, int k, int n, void *xq, float *xd, hipStream_t s) {
@@ -104,159 +159,13 @@ int launch_q4_quantize(const float *x, int k, int n, void *xq, float *xd, hipStr
   return VSIM_OK;
 }
 
-// ------------------------------------------------------------------ exact GEMV
-// y[ic][r] = the reference's sequential float chain (imax.c:1191-1229):
-//   for blocks i, bytes j: f0 = d0*(lo-8), f1 = d0*(hi-8), f2/f3 = xd; s += f0*f2 + f1*f3
-// One lane owns one (row, token) chain; the chain order is the reference's.
-template <int NT>
-__global__ void __launch_bounds__(256) k_gemv_exact(Q4View W, const float *__restrict__ xd, int n,
-                                                     const float *__restrict__ bias, float *__restrict__ y) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= W.rows) return;
-  const int nb = W.nb();
-  const int K = W.k;
-  const uint4 *qrow = (const uint4 *)(W.qs + (size_t)r * nb * 16);
-  const float *drow = W.d + (size_t)r * nb;
-  for (int ic0 = 0; ic0 < n; ic0 += NT) {
-    float acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = 0.0f;
-    for (int i = 0; i < nb; ++i) {
-      const float d0 = drow[i];
-      const uint4 q = qrow[i];
-      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) {
-#pragma unroll
-        for (int bj = 0; bj < 4; ++bj) {
-          const uint32_t byte = (qw[wv] >> (8 * bj)) & 0xFF;
-          const float f0 = d0 * (float)((int)(byte & 0xF) - 8);
-          const float f1 = d0 * (float)((int)(byte >> 4) - 8);
-          const int e = i * QK + 2 * (wv * 4 + bj);
-#pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            if (ic0 + t < n) {
-              const float2 a = *(const float2 *)(xd + (size_t)(ic0 + t) * K + e);
-              acc[t] = acc[t] + (f0 * a.x + f1 * a.y);
-            }
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      if (ic0 + t < n) y[(size_t)(ic0 + t) * W.rows + r] = bias ? acc[t] + bias[r] : acc[t];
-  }
-}
-
-// ------------------------------------------------------------------ fast GEMV
-// Same operands, HBM-streaming form: one wave per row, lanes stride over 16-byte nibble
-// blocks (1 KiB coalesced per wave-instruction), integer block dot with v_dot8_i32_i4 on
-// (nibble ^ 8) == signed (q - 8), then d0*d1*isum accumulated in fp32 and reduced across
-// the wave.  Different rounding from the reference chain (not bit-exact).
-template <int NT>
-__global__ void __launch_bounds__(256) k_gemv_fast(Q4View W, const uint8_t *__restrict__ xqs,
-                                                    const float *__restrict__ xdd, int n,
-                                                    const float *__restrict__ bias, float *__restrict__ y) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (r >= W.rows) return;
-  const int nb = W.nb();
-  const uint4 *qrow = (const uint4 *)(W.qs + (size_t)r * nb * 16);
-  const float *drow = W.d + (size_t)r * nb;
-  for (int ic0 = 0; ic0 < n; ic0 += NT) {
-    float acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = 0.0f;
-    for (int i = lane; i < nb; i += 64) {
-      const uint4 q = qrow[i];
-      const float d0 = drow[i];
-      const int a0 = (int)(q.x ^ 0x88888888u), a1 = (int)(q.y ^ 0x88888888u);
-      const int a2 = (int)(q.z ^ 0x88888888u), a3 = (int)(q.w ^ 0x88888888u);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (ic0 + t < n) {
-          const size_t xb = (size_t)(ic0 + t) * nb + i;
-          const uint4 xv = *(const uint4 *)(xqs + xb * 16);
-          int s = __builtin_amdgcn_sdot8(a0, (int)(xv.x ^ 0x88888888u), 0, false);
-          s = __builtin_amdgcn_sdot8(a1, (int)(xv.y ^ 0x88888888u), s, false);
-          s = __builtin_amdgcn_sdot8(a2, (int)(xv.z ^ 0x88888888u), s, false);
-          s = __builtin_amdgcn_sdot8(a3, (int)(xv.w ^ 0x88888888u), s, false);
-          acc[t] = __builtin_fmaf(d0 * xdd[xb], (float)s, acc[t]);
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const float v = wave_sum_f(acc[t]);
-      if (lane == 0 && ic0 + t < n) y[(size_t)(ic0 + t) * W.rows + r] = bias ? v + bias[r] : v;
-    }
-  }
-}
-
-int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias, float *y,
-                   int mode, hipStream_t s) {
-  if (K % QK || M <= 0 || n <= 0) { set_error("q4_gemv: bad shape"); return VSIM_EINVAL; }
-  const Q4View W = q4_view(w, M, K);
-  if (mode == VSIM_MODE_EXACT) {
-    if (!xd) { set_error("q4_gemv: exact mode needs xd"); return VSIM_EINVAL; }
-    hipLaunchKernelGGL(k_gemv_exact<1>, dim3((M + 255) / 256), dim3(256), 0, s, W, xd, n, bias, y);
-  } else {
-    const size_t nbk = (size_t)n * (K / QK);
-    const uint8_t *xqs = (const uint8_t *)xq;
-    const float *xdd = (const float *)(xqs + nbk * 16);
-    if (n == 1)
-      hipLaunchKernelGGL(k_gemv_fast<1>, dim3((M + 3) / 4), dim3(256), 0, s, W, xqs, xdd, n, bias, y);
-    else
-      hipLaunchKernelGGL(k_gemv_fast<4>, dim3((M + 3) / 4), dim3(256), 0, s, W, xqs, xdd, n, bias, y);
-  }
-  VSIM_HIP(hipGetLastError());
-  return VSIM_OK;
-}
-
-// ------------------------------------------------------------------ get_rows
-__global__ void k_get_rows(Q4View W, const int32_t *__restrict__ rows, int n, float *__restrict__ y) {
-  const int nb = W.nb();
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb * n) return;
-  const int t = b / nb, i = b % nb;
-  const int r = rows[t];
-  if (r < 0 || r >= W.rows) {  // the reference would read out of bounds; we emit NaN
-    for (int l = 0; l < QK; ++l) y[(size_t)t * W.k + i * QK + l] = __builtin_nanf("");
-    return;
-  }
-  const float d = W.d[(size_t)r * nb + i];
-  const uint4 q = *(const uint4 *)(W.qs + ((size_t)r * nb + i) * 16);
-  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-  float *o = y + (size_t)t * W.k + i * QK;
-#pragma unroll
-  for (int wv = 0; wv < 4; ++wv)
-#pragma unroll
-    for (int bj = 0; bj < 4; ++bj) {
-      const uint32_t byte = (qw[wv] >> (8 * bj)) & 0xFF;
-      o[2 * (wv * 4 + bj)] = (float)((int)(byte & 0xF) - 8) * d;
-      o[2 * (wv * 4 + bj) + 1] = (float)((int)(byte >> 4) - 8) * d;
-    }
-}
-
-int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s) {
-  if (K % QK || n <= 0) { set_error("get_rows: bad shape"); return VSIM_EINVAL; }
-  const Q4View W = q4_view(w, V, K);
-  const int nbk = n * (K / QK);
-  hipLaunchKernelGGL(k_get_rows, dim3((nbk + 127) / 128), dim3(128), 0, s, W, rows, n, y);
-  VSIM_HIP(hipGetLastError());
-  return VSIM_OK;
-}
-
-// ------------------------------------------------------------------ dequantize (SoA)
-// xd[r][e] = d*(q-8) for every element: the activation factors of the exact dot when the
-// quantized rows arrive from the host already quantized (the drop-in path).
-__global__ void k_q4_dequant(Q4View X, float *__restrict__ y) {
-  const int nb = X.nb();
+// xd[r][e] = d*(q-8): activation factors of rows that arrive already quantized (drop-in)
+__global__ void k_q4_dequant(const uint8_t *__restrict__ qs, const float *__restrict__ dd, size_t nblocks,
+                             float *__restrict__ y) {
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= (size_t)nb * X.rows) return;
-  const float d = X.d[b];
-  const uint4 q = *(const uint4 *)(X.qs + b * 16);
+  if (b >= nblocks) return;
+  const float d = dd[b];
+  const uint4 q = *(const uint4 *)(qs + b * 16);
   const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
   float *o = y + b * QK;
 #pragma unroll
@@ -269,10 +178,247 @@ __global__ void k_q4_dequant(Q4View X, float *__restrict__ y) {
     }
 }
 
-int launch_q4_dequant(const void *soa, int rows, int k, float *y, hipStream_t s) {
-  const Q4View X = q4_view(soa, rows, k);
+int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s) {
   const size_t nbk = (size_t)rows * (k / QK);
-  hipLaunchKernelGGL(k_q4_dequant, dim3((unsigned)((nbk + 127) / 128)), dim3(128), 0, s, X, y);
+  const uint8_t *qs = (const uint8_t *)xq;
+  const float *d = (const float *)(qs + nbk * 16);
+  hipLaunchKernelGGL(k_q4_dequant, dim3((unsigned)((nbk + 127) / 128)), dim3(128), 0, s, qs, d, nbk, y);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ pair products
+// The reference's per-byte term (imax.c:1219-1226): f0 = d0*(lo-8), f1 = d0*(hi-8),
+// p = f0*f2 + f1*f3, every product and the sum rounded separately (no FMA).  Nibbles of
+// four bytes are isolated with one AND and converted with v_cvt_f32_ubyteN.
+__device__ __forceinline__ void pair_terms4(uint32_t w, float d0, const float *x8, float *p4) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float f0 = d0 * ((float)((lo >> (8 * k)) & 0xFF) - 8.0f);
+    const float f1 = d0 * ((float)((hi >> (8 * k)) & 0xFF) - 8.0f);
+    p4[k] = f0 * x8[2 * k] + f1 * x8[2 * k + 1];
+  }
+}
+
+// ------------------------------------------------------------------ exact GEMV (N tokens)
+// One lane per (row, token) chain, reference order.  Used for prompt batches (N > 1).
+__global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__restrict__ xd, int n,
+                                                          const float *__restrict__ bias, float *__restrict__ y) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ic = blockIdx.y;
+  if (r >= W.rows || ic >= n) return;
+  const int nb = W.nb();
+  const float *xr = xd + (size_t)ic * W.k;
+  float acc = 0.0f;
+  for (int i = 0; i < nb; ++i) {
+    const size_t o = W.off(r, i);
+    const float d0 = W.d[o];
+    const uint4 q = *(const uint4 *)(W.qs + o * 16);
+    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) {
+      const float4 a = *(const float4 *)(xr + i * QK + wv * 8);
+      const float4 b = *(const float4 *)(xr + i * QK + wv * 8 + 4);
+      const float x8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      float p4[4];
+      pair_terms4(qw[wv], d0, x8, p4);
+      acc = acc + p4[0];
+      acc = acc + p4[1];
+      acc = acc + p4[2];
+      acc = acc + p4[3];
+    }
+  }
+  y[(size_t)ic * W.rows + r] = bias ? acc + bias[r] : acc;
+}
+
+// ------------------------------------------------------------------ exact GEMV (decode)
+// Producer/consumer over one 32-row tile and the whole K (the chain order forbids
+// splitting K).  Producer waves turn a chunk of C blocks x 32 rows into pair values
+// p[r][j] in LDS (all the VALU work, in parallel); the consumer wave adds them into the
+// 32 row chains in the reference order, one dependent add per pair, while the producers
+// fill the other LDS slot.  Layout [slot][row][pair] with a 4-float pad: producer
+// ds_write_b128 (8-lane groups on distinct 4-bank groups) and consumer ds_read_b128
+// (16-lane groups covering all 64 banks) are conflict-free.
+template <int C, int NPW>
+__global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_pc(GemvBatch B) {
+  constexpr int CP = C * 16;  // pairs per row per chunk
+  constexpr int LD = CP + 4;  // padded row stride (floats)
+  __shared__ __attribute__((aligned(16))) float P[2][T32 * LD];
+  int t = blockIdx.x, ji = 0;
+  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
+  const GemvJob J = B.j[ji];
+  const int nb = J.w.nb();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nchunks = (nb + C - 1) / C;
+  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
+  const float *dd = J.w.d + (size_t)t * nb * T32;
+  float s = 0.0f;
+  for (int c = 0; c <= nchunks; ++c) {
+    if (wave > 0 && c < nchunks) {
+      float *Ps = P[c & 1];
+      for (int i = (wave - 1) * 64 + lane; i < T32 * C; i += NPW * 64) {
+        const int r = i & (T32 - 1), b = i / T32;
+        const int blk = c * C + b;
+        if (blk < nb) {
+          const size_t o = (size_t)blk * T32 + r;
+          const float d0 = dd[o];
+          const uint4 q = *(const uint4 *)(qs + o * 16);
+          const float4 *xv = (const float4 *)(J.xd + (size_t)blk * QK);
+          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+          float4 *dst = (float4 *)(Ps + r * LD + b * 16);
+#pragma unroll
+          for (int wv = 0; wv < 4; ++wv) {
+            const float4 a = xv[2 * wv], bb = xv[2 * wv + 1];
+            const float x8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
+            float p4[4];
+            pair_terms4(qw[wv], d0, x8, p4);
+            dst[wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
+          }
+        }
+      }
+    }
+    if (wave == 0 && c > 0 && lane < T32) {
+      const float *pr = P[(c - 1) & 1] + lane * LD;
+      const int np = min(C, nb - (c - 1) * C) * 16;
+      if (np == CP) {
+#pragma unroll
+        for (int j = 0; j < CP; j += 4) {
+          const float4 v = *(const float4 *)(pr + j);
+          s = s + v.x;
+          s = s + v.y;
+          s = s + v.z;
+          s = s + v.w;
+        }
+      } else {
+        for (int j = 0; j < np; j += 4) {
+          const float4 v = *(const float4 *)(pr + j);
+          s = s + v.x;
+          s = s + v.y;
+          s = s + v.z;
+          s = s + v.w;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && lane < T32) {
+    const int row = t * T32 + lane;
+    if (row < J.w.rows) J.y[row] = J.bias ? s + J.bias[row] : s;
+  }
+}
+
+// ------------------------------------------------------------------ fast GEMV
+// HBM-streaming form of the same product: one 512-thread workgroup per 32-row tile, lane
+// (r, h) = (lane & 31, lane >> 5) of wave w streams blocks b = 2w + h, +16, ... (each
+// wave-instruction reads 1 KiB contiguous), integer block dot with v_dot8_i32_i4 on
+// (nibble ^ 8) == signed (q - 8), d0*d1*isum accumulated in fp32; 16 partials per row
+// summed through LDS in a fixed order (deterministic).  Not bit-exact to the reference.
+constexpr int FAST_WAVES = 8;
+__global__ void __launch_bounds__(64 * FAST_WAVES) k_gemv_fast(GemvBatch B) {
+  __shared__ float part[FAST_WAVES * 2][T32];
+  int t = blockIdx.x, ji = 0;
+  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
+  const GemvJob J = B.j[ji];
+  const int nb = J.w.nb();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & (T32 - 1), h = lane >> 5;
+  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
+  const float *dd = J.w.d + (size_t)t * nb * T32;
+  float acc = 0.0f;
+  for (int b = 2 * wave + h; b < nb; b += 2 * FAST_WAVES) {
+    const size_t o = (size_t)b * T32 + r;
+    const uint4 q = *(const uint4 *)(qs + o * 16);
+    const float d0 = dd[o];
+    const uint4 xv = *(const uint4 *)(J.xqs + (size_t)b * 16);
+    int sdot = __builtin_amdgcn_sdot8((int)(q.x ^ 0x88888888u), (int)(xv.x ^ 0x88888888u), 0, false);
+    sdot = __builtin_amdgcn_sdot8((int)(q.y ^ 0x88888888u), (int)(xv.y ^ 0x88888888u), sdot, false);
+    sdot = __builtin_amdgcn_sdot8((int)(q.z ^ 0x88888888u), (int)(xv.z ^ 0x88888888u), sdot, false);
+    sdot = __builtin_amdgcn_sdot8((int)(q.w ^ 0x88888888u), (int)(xv.w ^ 0x88888888u), sdot, false);
+    acc = __builtin_fmaf(d0 * J.xdd[b], (float)sdot, acc);
+  }
+  part[2 * wave + h][r] = acc;
+  __syncthreads();
+  if (threadIdx.x < T32) {
+    float sum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2 * FAST_WAVES; ++i) sum += part[i][threadIdx.x];
+    const int row = t * T32 + threadIdx.x;
+    if (row < J.w.rows) J.y[row] = J.bias ? sum + J.bias[row] : sum;
+  }
+}
+
+int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
+  int tiles = 0;
+  for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
+  if (tiles == 0) return VSIM_OK;
+  if (mode == VSIM_MODE_EXACT) {
+    hipLaunchKernelGGL((k_gemv_exact_pc<8, 4>), dim3(tiles), dim3(64 * 5), 0, s, B);
+  } else {
+    hipLaunchKernelGGL(k_gemv_fast, dim3(tiles), dim3(64 * FAST_WAVES), 0, s, B);
+  }
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias, float *y,
+                   int mode, hipStream_t s) {
+  if (K % QK || M <= 0 || n <= 0) { set_error("q4_gemv: bad shape"); return VSIM_EINVAL; }
+  const W4 W = w4_view(w, M, K);
+  if (mode == VSIM_MODE_EXACT && !xd) { set_error("q4_gemv: exact mode needs xd"); return VSIM_EINVAL; }
+  if (mode == VSIM_MODE_EXACT && n > 1) {
+    hipLaunchKernelGGL(k_gemv_exact_rows, dim3((M + 255) / 256, n), dim3(256), 0, s, W, xd, n, bias, y);
+    VSIM_HIP(hipGetLastError());
+    return VSIM_OK;
+  }
+  const size_t nbk = (size_t)n * (K / QK);
+  const uint8_t *xqs = (const uint8_t *)xq;
+  const float *xdd = (const float *)(xqs + nbk * 16);
+  for (int ic = 0; ic < n; ++ic) {
+    GemvBatch B{};
+    B.nj = 1;
+    B.j[0].w = W;
+    B.j[0].xd = xd ? xd + (size_t)ic * K : nullptr;
+    B.j[0].xqs = xqs + (size_t)ic * (K / QK) * 16;
+    B.j[0].xdd = xdd + (size_t)ic * (K / QK);
+    B.j[0].bias = bias;
+    B.j[0].y = y + (size_t)ic * M;
+    if (int rc = launch_gemv_batch(B, mode, s)) return rc;
+  }
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ get_rows
+__global__ void k_get_rows(W4 W, const int32_t *__restrict__ rows, int n, float *__restrict__ y) {
+  const int nb = W.nb();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb * n) return;
+  const int t = b / nb, i = b % nb;
+  const int r = rows[t];
+  float *o = y + (size_t)t * W.k + i * QK;
+  if (r < 0 || r >= W.rows) {  // the reference would read out of bounds; we emit NaN
+    for (int l = 0; l < QK; ++l) o[l] = __builtin_nanf("");
+    return;
+  }
+  const size_t off = W.off(r, i);
+  const float d = W.d[off];
+  const uint4 q = *(const uint4 *)(W.qs + off * 16);
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int wv = 0; wv < 4; ++wv)
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj) {
+      const uint32_t byte = (qw[wv] >> (8 * bj)) & 0xFF;
+      o[2 * (wv * 4 + bj)] = (float)((int)(byte & 0xF) - 8) * d;
+      o[2 * (wv * 4 + bj) + 1] = (float)((int)(byte >> 4) - 8) * d;
+    }
+}
+
+int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s) {
+  if (K % QK || n <= 0) { set_error("get_rows: bad shape"); return VSIM_EINVAL; }
+  const W4 W = w4_view(w, V, K);
+  const int nbk = n * (K / QK);
+  hipLaunchKernelGGL(k_get_rows, dim3((nbk + 127) / 128), dim3(128), 0, s, W, rows, n, y);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -290,27 +436,21 @@ __device__ __forceinline__ float randn(uint64_t seed, uint64_t i) {
   return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
 }
 
-__global__ void k_randn_q4(uint8_t *__restrict__ qs, float *__restrict__ dd, size_t nblocks, uint64_t seed, float sd) {
-  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
+__global__ void k_randn_w4(W4 W, uint64_t seed, float sd) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = W.nb();
+  if (i >= (size_t)W.tiles * T32 * nb) return;
+  const int r = (int)(i / nb), b = (int)(i % nb);
+  const size_t o = W.off(r, b);
+  if (r >= W.rows) {
+    ((float *)W.d)[o] = 0.0f;
+    *(uint4 *)(W.qs + o * 16) = make_uint4(0x88888888u, 0x88888888u, 0x88888888u, 0x88888888u);
+    return;
+  }
   float v[QK];
-  float amax = 0.0f;
 #pragma unroll
-  for (int l = 0; l < QK; ++l) {
-    v[l] = randn(seed, b * QK + l) * sd;
-    amax = amax > fabsf(v[l]) ? amax : fabsf(v[l]);
-  }
-  const float d = amax / 7.0f;
-  const float id = d != 0.0f ? 1.0f / d : 0.0f;
-  uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int l = 0; l < QK; l += 2) {
-    const int q0 = (int)(int8_t)roundf(v[l] * id) + 8;
-    const int q1 = (int)(int8_t)roundf(v[l + 1] * id) + 8;
-    w[l / 8] |= (uint32_t)((q0 & 0xF) | ((q1 & 0xF) << 4)) << (8 * ((l / 2) & 3));
-  }
-  *(uint4 *)(qs + b * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-  dd[b] = d;
+  for (int l = 0; l < QK; ++l) v[l] = randn(seed, i * QK + l) * sd;
+  quantize_block(v, (uint8_t *)W.qs + o * 16, (float *)W.d + o, nullptr);
 }
 
 __global__ void k_randn_f32(float *x, int n, uint64_t seed, float sd, float mean) {
@@ -318,11 +458,10 @@ __global__ void k_randn_f32(float *x, int n, uint64_t seed, float sd, float mean
   if (i < n) x[i] = mean + randn(seed, (uint64_t)i) * sd;
 }
 
-int launch_randn_q4(void *soa, int rows, int k, uint64_t seed, float stddev, hipStream_t s) {
-  const size_t nbk = (size_t)rows * (k / QK);
-  uint8_t *qs = (uint8_t *)soa;
-  float *d = (float *)(qs + nbk * 16);
-  hipLaunchKernelGGL(k_randn_q4, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, qs, d, nbk, seed, stddev);
+int launch_randn_q4(void *w, int rows, int k, uint64_t seed, float stddev, hipStream_t s) {
+  const W4 W = w4_view(w, rows, k);
+  const size_t tot = (size_t)W.tiles * T32 * W.nb();
+  hipLaunchKernelGGL(k_randn_w4, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, W, seed, stddev);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

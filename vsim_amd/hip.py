@@ -26,7 +26,8 @@ EXPORTS = [
     "init_xmax", "imax_ggml_compute_forward_mul_mat_q4_0_f32",
     "vsim_ggml_gptneox_rope_f32", "vsim_ggml_rope_f32", "vsim_ggml_soft_max_f32", "vsim_ggml_mul_mat_f32",
     "vsim_dropin_stats", "vsim_dropin_reset",
-    "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_get_rows",
+    "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_act_repack", "vsim_op_act_unpack",
+    "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_get_rows",
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
     "vsim_op_tables",
     "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_randomize",
@@ -61,6 +62,8 @@ def lib():
     L.vsim_q4_bytes.argtypes = [ci, ci]
     L.vsim_op_q4_repack.argtypes = [vp, vp, ci, ci, vp]
     L.vsim_op_q4_unpack.argtypes = [vp, vp, ci, ci, vp]
+    L.vsim_op_act_repack.argtypes = [vp, vp, ci, ci, vp]
+    L.vsim_op_act_unpack.argtypes = [vp, vp, ci, ci, vp]
     L.vsim_op_q4_quantize.argtypes = [vp, ci, ci, vp, vp, vp]
     L.vsim_op_q4_gemv.argtypes = [vp, ci, ci, vp, vp, ci, vp, vp, ci, vp]
     L.vsim_op_get_rows.argtypes = [vp, ci, ci, vp, ci, vp, vp]
