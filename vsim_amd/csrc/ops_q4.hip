@@ -353,7 +353,18 @@ int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
   for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
   if (tiles == 0) return VSIM_OK;
   if (mode == VSIM_MODE_EXACT) {
-    hipLaunchKernelGGL((k_gemv_exact_pc<8, 4>), dim3(tiles), dim3(64 * 5), 0, s, B);
+    static int variant = [] {
+      const char *e = getenv("VSIM_GEMV_PC");
+      return e ? atoi(e) : 0;
+    }();
+    switch (variant) {  // tuning knob: chunk blocks C x producer waves NPW
+      case 1: hipLaunchKernelGGL((k_gemv_exact_pc<4, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
+      case 2: hipLaunchKernelGGL((k_gemv_exact_pc<16, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
+      case 3: hipLaunchKernelGGL((k_gemv_exact_pc<8, 3>), dim3(tiles), dim3(64 * 4), 0, s, B); break;
+      case 4: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
+      case 5: hipLaunchKernelGGL((k_gemv_exact_pc<16, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
+      default: hipLaunchKernelGGL((k_gemv_exact_pc<8, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
+    }
   } else {
     hipLaunchKernelGGL(k_gemv_fast, dim3(tiles), dim3(64 * FAST_WAVES), 0, s, B);
   }
