@@ -33,6 +33,19 @@ def main():
         xd = torch.empty(K, device="cuda")
         y = torch.empty(M, device="cuda")
         hip.check(L.vsim_op_q4_quantize(x.data_ptr(), K, 1, xq.data_ptr(), xd.data_ptr(), None))
+        # bit-exactness of the decode kernel vs the row-per-lane kernel (n = 2 path)
+        x2 = torch.cat([x, x])
+        xq2 = torch.empty(hip.q4_bytes(2, K), dtype=torch.uint8, device="cuda")
+        xd2 = torch.empty(2 * K, device="cuda")
+        y2 = torch.empty(2 * M, device="cuda")
+        hip.check(L.vsim_op_q4_quantize(x2.data_ptr(), K, 2, xq2.data_ptr(), xd2.data_ptr(), None))
+        hip.check(L.vsim_op_q4_gemv(w.data_ptr(), M, K, xq2.data_ptr(), xd2.data_ptr(), 2, None, y2.data_ptr(),
+                                    hip.MODE_EXACT, None))
+        hip.check(L.vsim_op_q4_gemv(w.data_ptr(), M, K, xq.data_ptr(), xd.data_ptr(), 1, None, y.data_ptr(),
+                                    hip.MODE_EXACT, None))
+        torch.cuda.synchronize()
+        same = torch.equal(y.view(torch.int32), y2[:M].view(torch.int32))
+        print(f"{name:16s} exact decode kernel bit-identical to row kernel: {same}", flush=True)
         for mode in (hip.MODE_EXACT, hip.MODE_FAST):
             for _ in range(3):
                 hip.check(L.vsim_op_q4_gemv(w.data_ptr(), M, K, xq.data_ptr(), xd.data_ptr(), 1, None, y.data_ptr(),
