@@ -232,6 +232,24 @@ __global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__re
   y[(size_t)ic * W.rows + r] = bias ? acc + bias[r] : acc;
 }
 
+// Consumer step: add one full chunk of pairs into the chain.  All LDS reads are issued
+// before the first add (the hardware keeps up to 15 in flight), so the dependent add
+// chain does not stall on each read's latency.
+template <int CP>
+__device__ __forceinline__ float chain_chunk(const float *pr, float s) {
+  float4 v[CP / 4];
+#pragma unroll
+  for (int j = 0; j < CP / 4; ++j) v[j] = *(const float4 *)(pr + 4 * j);
+#pragma unroll
+  for (int j = 0; j < CP / 4; ++j) {
+    s = s + v[j].x;
+    s = s + v[j].y;
+    s = s + v[j].z;
+    s = s + v[j].w;
+  }
+  return s;
+}
+
 // ------------------------------------------------------------------ exact GEMV (decode)
 // Producer/consumer over one 32-row tile and the whole K (the chain order forbids
 // splitting K).  Producer waves turn a chunk of C blocks x 32 rows into pair values
@@ -282,14 +300,7 @@ __global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_pc(GemvBatch B) {
       const float *pr = P[(c - 1) & 1] + lane * LD;
       const int np = min(C, nb - (c - 1) * C) * 16;
       if (np == CP) {
-#pragma unroll
-        for (int j = 0; j < CP; j += 4) {
-          const float4 v = *(const float4 *)(pr + j);
-          s = s + v.x;
-          s = s + v.y;
-          s = s + v.z;
-          s = s + v.w;
-        }
+        s = chain_chunk<CP>(pr, s);
       } else {
         for (int j = 0; j < np; j += 4) {
           const float4 v = *(const float4 *)(pr + j);
@@ -347,14 +358,7 @@ __global__ void __launch_bounds__(64 * (1 + NP)) k_gemv_exact_v2(GemvBatch B) {
         const float *pr = P[slot] + lane * LD;
         const int np = min(C, nb - c * C) * 16;
         if (np == CP) {
-#pragma unroll
-          for (int j = 0; j < CP; j += 4) {
-            const float4 v = *(const float4 *)(pr + j);
-            s = s + v.x;
-            s = s + v.y;
-            s = s + v.z;
-            s = s + v.w;
-          }
+          s = chain_chunk<CP>(pr, s);
         } else {
           for (int j = 0; j < np; j += 4) {
             const float4 v = *(const float4 *)(pr + j);
