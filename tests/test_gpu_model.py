@@ -132,3 +132,27 @@ def test_pipeline_stages_equal_single_stage(tmp_path):
         assert np.array_equal(lp.view(np.uint32), lf.view(np.uint32)), step
         n_past += len(ids)
         ids = [int(np.argmax(lf))]
+
+
+@pytest.mark.parametrize("cfg", ["small-gptj", "small-neox"])
+def test_graph_replay_bit_exact_vs_oracle(cfg, tmp_path):
+    """The decode step captured once in a hipGraph and replayed (n_past and the token read
+    from device memory) gives the oracle's logits at every step."""
+    import oracle_py as O
+    arch_s, hp = mg.CONFIGS[cfg]
+    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    path = str(tmp_path / f"{cfg}.bin")
+    mg.write_model(path, arch_s, hp, seed=8, std=0.05)
+    om = O.Model(path, arch)
+    dm = hip.Model.load(path, arch)
+    dm.set_graph(True)
+    ids = [4, 8, 15, 16, 23, 42]
+    lo, ld = om.eval(0, ids), dm.eval(0, ids)
+    assert np.array_equal(lo.view(np.uint32), ld.view(np.uint32))
+    n_past = len(ids)
+    for step in range(24):
+        t = int(np.argmax(lo))
+        lo, ld = om.eval(n_past, [t]), dm.eval(n_past, [t])
+        assert np.array_equal(lo.view(np.uint32), ld.view(np.uint32)), step
+        n_past += 1
+    assert dm.info()["graph"]

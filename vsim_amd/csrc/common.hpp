@@ -48,6 +48,11 @@ inline W4 w4_view(const void *base, int rows, int k) {
 // A batch of up to 4 independent GEMVs (same token) in one launch; workgroups take the
 // tiles of job 0, then job 1, ...  Activation operands: xd = dequantized factors (exact
 // mode), xqs/xdd = Q4_0 nibbles and scales of the activation row (fast mode).
+// Epilogues: EPI_STORE y[row] = dot (+ bias[row]); EPI_GELU_Q: g = gelu_lut(dot + bias)
+// (vsim.cpp:680-683), y[row] = g if y != NULL, and the tile's 32 values — block `tile` of
+// the next product's activation row — are quantized with quantize_row_q4_0 semantics into
+// (oq_qs, oq_d, oxd) (the INIT-phase quantization of the following mul_mat, ggml.c:5024).
+enum { EPI_STORE = 0, EPI_GELU_Q = 1 };
 struct GemvJob {
   W4 w;
   const float *xd;
@@ -55,11 +60,55 @@ struct GemvJob {
   const float *xdd;
   const float *bias;
   float *y;
+  int epi;
+  const uint16_t *gelu_tab;
+  uint8_t *oq_qs;
+  float *oq_d;
+  float *oxd;
 };
 struct GemvBatch {
   GemvJob j[4];
   int nj;
 };
+
+// ---------------------------------------------------------------- fused decode kernels
+// (layer.hip)
+struct LnQuantJob {
+  const float *x;      // [n] input row
+  const float *w, *b;  // affine (non-null)
+  uint8_t *qs;         // [n/32][16]
+  float *d;            // [n/32]
+  float *xd;           // [n]
+};
+
+// Rows [32t, 32t+32) of the out-projection (a) and of fc_out (b) in one workgroup, epilogue
+// inpL[row] = inpL[row] + ((a + bias_a) + (b + bias_b))  (vsim.cpp:694-695).
+struct DualJob {
+  W4 a, b;
+  const float *xda, *xdb;        // exact operands
+  const uint8_t *xqa, *xqb;      // fast operands (nibbles)
+  const float *xdda, *xddb;      // fast operands (scales)
+  const float *bias_a, *bias_b;  // bias_a may be NULL (GPT-J out_proj has none)
+  float *inpL;
+};
+
+struct AttnJob {
+  const float *q, *k, *v;  // new rows [E] (Q, K, V after bias)
+  float *kc, *vc;          // this layer's cache, [n_ctx][E]
+  const int *npast;        // device scalar
+  const double2 *cs;       // RoPE cos/sin table [n_ctx][n_rot/2]
+  const uint16_t *etab;    // table_exp_f16
+  int d, H, n_rot, style;  // style 0 = GPT-NeoX rotate-half, 1 = GPT-J pairs
+  float scale;
+  uint8_t *oq_qs;          // output activation, Q4 SoA (E/32 blocks)
+  float *oq_d, *oxd;
+  float *out;              // optional float copy [E]
+};
+
+int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s);
+int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s);
+int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s);
+int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s);
 
 // ---------------------------------------------------------------- fp16 (ggml.c:95-142)
 __device__ __forceinline__ float bits_f(uint32_t w) { return __uint_as_float(w); }

@@ -1,0 +1,212 @@
+// vsim_amd/csrc/kern.hpp — device building blocks shared by the kernel files.
+#pragma once
+
+#include "common.hpp"
+
+namespace vsim {
+
+// ------------------------------------------------------------------ activation quantize
+// One thread per 32-block.  Bit-identical to quantize_row_q4_0: fp32 amax, d = amax/7
+// (correctly rounded division), id = 1/d, q = (int8)round(x*id) + 8 with round-half-
+// away-from-zero, nibble pairs (q[2l], q[2l+1]).  Also emits xd = d*(q-8) per element,
+// the activation factor f2/f3 of the reference dot (ggml.c:497-498).
+__device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, float *d_out, float *xd_out) {
+  float amax = 0.0f;
+#pragma unroll
+  for (int l = 0; l < QK; ++l) amax = amax > fabsf(v[l]) ? amax : fabsf(v[l]);
+  const float d = amax / 7.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  uint32_t w[4] = {0, 0, 0, 0};
+  float out[QK];
+#pragma unroll
+  for (int l = 0; l < QK; l += 2) {
+    const int q0 = x86_round_i8(v[l] * id) + 8;
+    const int q1 = x86_round_i8(v[l + 1] * id) + 8;
+    w[l / 8] |= (uint32_t)((q0 & 0xF) | ((q1 & 0xF) << 4)) << (8 * ((l / 2) & 3));
+    out[l] = d * (float)(q0 - 8);
+    out[l + 1] = d * (float)(q1 - 8);
+  }
+  *(uint4 *)qs_out = make_uint4(w[0], w[1], w[2], w[3]);
+  *d_out = d;
+  if (xd_out) {
+    float4 *o = (float4 *)xd_out;
+#pragma unroll
+    for (int i = 0; i < QK / 4; ++i) o[i] = make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
+  }
+}
+
+// ------------------------------------------------------------------ pair products
+// The reference's per-byte term (imax.c:1219-1226): f0 = d0*(lo-8), f1 = d0*(hi-8),
+// p = f0*f2 + f1*f3, every product and the sum rounded separately (no FMA).  Nibbles of
+// four bytes are isolated with one AND and converted with v_cvt_f32_ubyteN.
+__device__ __forceinline__ void pair_terms4(uint32_t w, float d0, const float *x8, float *p4) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float f0 = d0 * ((float)((lo >> (8 * k)) & 0xFF) - 8.0f);
+    const float f1 = d0 * ((float)((hi >> (8 * k)) & 0xFF) - 8.0f);
+    p4[k] = f0 * x8[2 * k] + f1 * x8[2 * k + 1];
+  }
+}
+
+// Consumer step: add one full chunk of pairs into the chain.  All LDS reads are issued
+// before the first add (the hardware keeps up to 15 in flight), so the dependent add
+// chain does not stall on each read's latency.
+template <int CP>
+__device__ __forceinline__ float chain_chunk(const float *pr, float s) {
+  float4 v[CP / 4];
+#pragma unroll
+  for (int j = 0; j < CP / 4; ++j) v[j] = *(const float4 *)(pr + 4 * j);
+#pragma unroll
+  for (int j = 0; j < CP / 4; ++j) {
+    s = s + v[j].x;
+    s = s + v[j].y;
+    s = s + v[j].z;
+    s = s + v[j].w;
+  }
+  return s;
+}
+
+constexpr int NORM_THREADS = 256;
+
+__device__ __forceinline__ int ulp_exp(float x) {
+  const uint32_t b = __float_as_uint(x) & 0x7FFFFFFFu;
+  if (b == 0) return 1 << 30;
+  const int e = (int)(b >> 23);
+  return e == 0 ? -149 : e - 150;
+}
+
+template <typename T>
+__device__ T block_sum(T v, T *sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  T r = 0;
+  for (int w = 0; w < NORM_THREADS / 64; ++w) r += sh[w];
+  return r;
+}
+
+__device__ int block_min(int v, int *sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_min_i(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  int r = sh[0];
+  for (int w = 1; w < NORM_THREADS / 64; ++w) r = min(r, sh[w]);
+  return r;
+}
+
+
+}  // namespace vsim
+
+namespace vsim {
+
+// ------------------------------------------------------------------ exact LayerNorm core
+// ggml_compute_forward_norm_f32 (ggml.c:4246-4304) for one row by one 256-thread block,
+// result left in `row` (LDS, n floats, in place).  The reference sums sequentially in
+// double; we sum in parallel and prove the sum equal to the sequential one, falling back
+// to the sequential loop otherwise:
+//  * mean: every partial sum of floats that are multiples of 2^umin is exact in double
+//    while sum|x| < 2^(53+umin), so then any order gives the sequential value;
+//  * variance: sequential and tree sums of w_i = v_i^2 >= 0 differ by at most
+//    (2n+64)*2^-53*sum(w); if both ends of that interval give the same float scale
+//    (the map S -> (float)(1/sqrt(S/n+eps)) is monotone) the scale is the reference's.
+// Optional affine y = w*y + b (ggml_add(ggml_mul(repeat(w), cur), repeat(b))).
+// stats (optional): [0] mean fallbacks, [1] variance fallbacks.
+__device__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
+                             const float *__restrict__ gb, unsigned *stats) {
+  __shared__ double shd[NORM_THREADS / 64];
+  __shared__ int shi[NORM_THREADS / 64];
+  __shared__ double bcast_d;
+  __shared__ float bcast_f;
+  const double eps = 1e-5f;
+  double s = 0.0, sa = 0.0;
+  int um = 1 << 30;
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
+    const float v = x[i];
+    row[i] = v;
+    s += (double)v;
+    sa += (double)fabsf(v);
+    um = min(um, ulp_exp(v));
+  }
+  s = block_sum(s, shd);
+  sa = block_sum(sa, shd);
+  um = block_min(um, shi);
+  const bool exact = (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
+  if (!exact) {
+    if (threadIdx.x == 0) {
+      double m = 0.0;
+      for (int i = 0; i < n; ++i) m += row[i];
+      bcast_d = m;
+      if (stats) atomicAdd(&stats[0], 1u);
+    }
+    __syncthreads();
+    s = bcast_d;
+  }
+  const double mean = s / n;
+  double s2 = 0.0;
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
+    const double v = (double)row[i] - mean;
+    s2 += v * v;
+  }
+  s2 = block_sum(s2, shd);
+  const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
+  const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
+  const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
+  float scale = sc_lo;
+  if (sc_lo != sc_hi) {
+    if (threadIdx.x == 0) {
+      double q = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double v = (double)row[i] - mean;
+        q += v * v;
+      }
+      bcast_f = (float)(1.0 / sqrt(q / n + eps));
+      if (stats) atomicAdd(&stats[1], 1u);
+    }
+    __syncthreads();
+    scale = bcast_f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
+    float v = (float)((double)row[i] - mean);
+    v = v * scale;
+    if (gw) v = (gw[i] * v) + gb[i];
+    row[i] = v;
+  }
+  __syncthreads();
+}
+
+// Quantize one 32-element block held by lanes 0..31 of a wave (value v in lane l = element
+// l): quantize_row_q4_0 semantics; writes the 16 nibble bytes, d and the 32 xd factors.
+// Must be called by all 64 lanes of the wave (lanes 32..63 pass v = 0 and write nothing).
+__device__ __forceinline__ void quantize_block_lanes(float v, int lane, uint8_t *qs_out, float *d_out,
+                                                     float *xd_out) {
+  float a = lane < 32 ? fabsf(v) : 0.0f;
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    const float t = __shfl_xor(a, o, 64);
+    a = a > t ? a : t;
+  }
+  const float amax = a;
+  const float d = amax / 7.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  const int q = x86_round_i8(v * id) + 8;
+  // byte j = q[2j] | q[2j+1] << 4 ; word w = bytes 4w..4w+3
+  const int qn = __shfl_xor(q, 1, 64);
+  const uint32_t byte = (lane & 1) ? 0u : (uint32_t)((q & 0xF) | ((qn & 0xF) << 4));
+  uint32_t word = byte << (8 * ((lane >> 1) & 3));
+  word |= __shfl_xor(word, 2, 64);
+  word |= __shfl_xor(word, 4, 64);
+  if (lane < 32) {
+    if ((lane & 7) == 0) ((uint32_t *)qs_out)[lane >> 3] = word;
+    if (lane == 0) *d_out = d;
+    xd_out[lane] = d * (float)(q - 8);
+  }
+}
+
+}  // namespace vsim

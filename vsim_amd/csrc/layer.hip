@@ -1,0 +1,428 @@
+// vsim_amd/csrc/layer.hip — fused kernels of the single-token decode step.
+//
+// One decoder layer = 4 launches (vsim.cpp:521-696 for GPT-NeoX with parallel residual,
+// the same ops for GPT-J):
+//   1. k_ln_quant      LayerNorm(s) + affine + activation quantization (ggml.c:4246,
+//                      5024-5041): inpL -> Q4_0 activation row(s) and their xd factors
+//   2. GEMV batch      {Q, K, V, fc_in} in one launch; fc_in's epilogue adds the bias, looks
+//                      up GELU and quantizes each 32-row tile into the fc_out activation
+//   3. k_attn_decode   per head: RoPE on q and the new k, KV-cache write, KQ (double
+//                      accumulator), scale/softmax (fp16 exp table), KQV (sequential float
+//                      mad), quantize the head's output for the out-projection
+//   4. dual GEMV       out-projection and fc_out for the same 32 rows in one workgroup,
+//                      epilogue inpL += (attn + ff)  (vsim.cpp:694-695)
+// Every value is computed with the reference's operation order and rounding (exact mode);
+// the fast mode swaps in the integer-dot GEMV bodies.  n_past is read from device memory so
+// the whole step can be captured once in a hipGraph and replayed per token.
+#include "kern.hpp"
+#include "../../include/vsim_hip.h"
+
+namespace vsim {
+
+extern unsigned *g_norm_stats;
+
+// ------------------------------------------------------------------ 1. LN + quantize
+__global__ void __launch_bounds__(NORM_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
+  extern __shared__ __attribute__((aligned(16))) float row[];
+  const LnQuantJob J = blockIdx.x == 0 ? j0 : j1;
+  ln_exact_lds(J.x, row, n, J.w, J.b, stats);
+  const int nb = n / QK;
+  for (int b = threadIdx.x; b < nb; b += NORM_THREADS) {
+    float v[QK];
+#pragma unroll
+    for (int l = 0; l < QK; ++l) v[l] = row[b * QK + l];
+    quantize_block(v, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
+  }
+}
+
+int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_ln_quant, dim3(j1 ? 2 : 1), dim3(NORM_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
+                     g_norm_stats);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ GEMV epilogues
+// Called by all 64 lanes of wave 0 with the row sums in lanes 0..31.
+__device__ __forceinline__ void gemv_epilogue(const GemvJob &J, int t, float s, int lane) {
+  const int row = t * T32 + lane;
+  if (J.epi == EPI_GELU_Q) {
+    float g = 0.0f;
+    if (lane < T32) {
+      const float v = s + J.bias[row];
+      g = h2f(J.gelu_tab[f2h(v)]);
+      if (J.y) J.y[row] = g;
+    }
+    quantize_block_lanes(g, lane, J.oq_qs + (size_t)t * 16, J.oq_d + t, J.oxd + (size_t)t * QK);
+  } else if (lane < T32 && row < J.w.rows) {
+    J.y[row] = J.bias ? s + J.bias[row] : s;
+  }
+}
+
+// ------------------------------------------------------------------ 2. exact GEMV + epilogues
+// Producer/consumer over one 32-row tile (see k_gemv_exact_pc in ops_q4.hip for the
+// decomposition); this version adds the job epilogues.
+template <int C, int NPW>
+__global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_epi(GemvBatch B) {
+  constexpr int CP = C * 16;
+  constexpr int LD = CP + 4;
+  __shared__ __attribute__((aligned(16))) float P[2][T32 * LD];
+  int t = blockIdx.x, ji = 0;
+  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
+  const GemvJob &J = B.j[ji];
+  const int nb = J.w.nb();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nchunks = (nb + C - 1) / C;
+  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
+  const float *dd = J.w.d + (size_t)t * nb * T32;
+  float s = 0.0f;
+  for (int c = 0; c <= nchunks; ++c) {
+    if (wave > 0 && c < nchunks) {
+      float *Ps = P[c & 1];
+      for (int i = (wave - 1) * 64 + lane; i < T32 * C; i += NPW * 64) {
+        const int r = i & (T32 - 1), b = i / T32;
+        const int blk = c * C + b;
+        if (blk < nb) {
+          const size_t o = (size_t)blk * T32 + r;
+          const float d0 = dd[o];
+          const uint4 q = *(const uint4 *)(qs + o * 16);
+          const float4 *xv = (const float4 *)(J.xd + (size_t)blk * QK);
+          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+          float4 *dst = (float4 *)(Ps + r * LD + b * 16);
+#pragma unroll
+          for (int wv = 0; wv < 4; ++wv) {
+            const float4 a = xv[2 * wv], bb = xv[2 * wv + 1];
+            const float x8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
+            float p4[4];
+            pair_terms4(qw[wv], d0, x8, p4);
+            dst[wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
+          }
+        }
+      }
+    }
+    if (wave == 0 && c > 0 && lane < T32) {
+      const float *pr = P[(c - 1) & 1] + lane * LD;
+      const int np = min(C, nb - (c - 1) * C) * 16;
+      if (np == CP) {
+        s = chain_chunk<CP>(pr, s);
+      } else {
+        for (int j = 0; j < np; j += 4) {
+          const float4 v = *(const float4 *)(pr + j);
+          s = s + v.x;
+          s = s + v.y;
+          s = s + v.z;
+          s = s + v.w;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) gemv_epilogue(J, t, s, lane);
+}
+
+// ------------------------------------------------------------------ fast GEMV + epilogues
+constexpr int FW = 8;  // waves per workgroup of the fast kernels
+__global__ void __launch_bounds__(64 * FW) k_gemv_fast_epi(GemvBatch B) {
+  __shared__ float part[FW * 2][T32];
+  int t = blockIdx.x, ji = 0;
+  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
+  const GemvJob &J = B.j[ji];
+  const int nb = J.w.nb();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & (T32 - 1), h = lane >> 5;
+  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
+  const float *dd = J.w.d + (size_t)t * nb * T32;
+  float acc = 0.0f;
+  for (int b = 2 * wave + h; b < nb; b += 2 * FW) {
+    const size_t o = (size_t)b * T32 + r;
+    const uint4 q = *(const uint4 *)(qs + o * 16);
+    const float d0 = dd[o];
+    const uint4 xv = *(const uint4 *)(J.xqs + (size_t)b * 16);
+    int sd = __builtin_amdgcn_sdot8((int)(q.x ^ 0x88888888u), (int)(xv.x ^ 0x88888888u), 0, false);
+    sd = __builtin_amdgcn_sdot8((int)(q.y ^ 0x88888888u), (int)(xv.y ^ 0x88888888u), sd, false);
+    sd = __builtin_amdgcn_sdot8((int)(q.z ^ 0x88888888u), (int)(xv.z ^ 0x88888888u), sd, false);
+    sd = __builtin_amdgcn_sdot8((int)(q.w ^ 0x88888888u), (int)(xv.w ^ 0x88888888u), sd, false);
+    acc = __builtin_fmaf(d0 * J.xdd[b], (float)sd, acc);
+  }
+  part[2 * wave + h][r] = acc;
+  __syncthreads();
+  if (wave == 0) {
+    float sum = 0.0f;
+    if (lane < T32) {
+#pragma unroll
+      for (int i = 0; i < 2 * FW; ++i) sum += part[i][lane];
+    }
+    gemv_epilogue(J, t, sum, lane);
+  }
+}
+
+int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s) {
+  int tiles = 0;
+  for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
+  if (mode == VSIM_MODE_EXACT)
+    hipLaunchKernelGGL((k_gemv_exact_epi<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B);
+  else
+    hipLaunchKernelGGL(k_gemv_fast_epi, dim3(tiles), dim3(64 * FW), 0, s, B);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ 4. dual GEMV + residual
+// Rows [32t, 32t+32) of the out-projection (A: K = E, input = attention output) and of
+// fc_out (B: K = 4E, input = quantized GELU output) in one workgroup; the consumer lanes run
+// both chains interleaved (two independent dependent chains share the add latency), then
+// inpL[row] = inpL[row] + ((A + biasA) + (B + biasB)).
+template <int C>
+__device__ __forceinline__ void produce_chunk(const W4 &w, int t, const float *xd, int c, float *Ps, int item, int LD) {
+  const int nb = w.nb();
+  const int r = item & (T32 - 1), b = item / T32;
+  const int blk = c * C + b;
+  if (blk >= nb) return;
+  const size_t o = ((size_t)t * nb + blk) * T32 + r;
+  const float d0 = w.d[o];
+  const uint4 q = *(const uint4 *)(w.qs + o * 16);
+  const float4 *xv = (const float4 *)(xd + (size_t)blk * QK);
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+  float4 *dst = (float4 *)(Ps + r * LD + b * 16);
+#pragma unroll
+  for (int wv = 0; wv < 4; ++wv) {
+    const float4 a = xv[2 * wv], bb = xv[2 * wv + 1];
+    const float x8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
+    float p4[4];
+    pair_terms4(qw[wv], d0, x8, p4);
+    dst[wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
+  }
+}
+
+template <int C, int NPW>
+__global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_dual(DualJob D) {
+  constexpr int CP = C * 16;
+  constexpr int LD = CP + 4;
+  __shared__ __attribute__((aligned(16))) float PA[2][T32 * LD];
+  __shared__ __attribute__((aligned(16))) float PB[2][T32 * LD];
+  const int t = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nca = (D.a.nb() + C - 1) / C, ncb = (D.b.nb() + C - 1) / C;
+  const int nch = max(nca, ncb);
+  float sa = 0.0f, sb = 0.0f;
+  for (int c = 0; c <= nch; ++c) {
+    if (wave > 0 && c < nch) {
+      for (int i = (wave - 1) * 64 + lane; i < 2 * T32 * C; i += NPW * 64) {
+        if (i < T32 * C) {
+          if (c < nca) produce_chunk<C>(D.a, t, D.xda, c, PA[c & 1], i, LD);
+        } else if (c < ncb) {
+          produce_chunk<C>(D.b, t, D.xdb, c, PB[c & 1], i - T32 * C, LD);
+        }
+      }
+    }
+    if (wave == 0 && c > 0 && lane < T32) {
+      const int cc = c - 1;
+      const float *pa = PA[cc & 1] + lane * LD;
+      const float *pb = PB[cc & 1] + lane * LD;
+      const int npa = cc < nca ? min(C, D.a.nb() - cc * C) * 16 : 0;
+      const int npb = cc < ncb ? min(C, D.b.nb() - cc * C) * 16 : 0;
+      if (npa == CP && npb == CP) {
+        float4 va[CP / 4], vb[CP / 4];
+#pragma unroll
+        for (int j = 0; j < CP / 4; ++j) {
+          va[j] = *(const float4 *)(pa + 4 * j);
+          vb[j] = *(const float4 *)(pb + 4 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < CP / 4; ++j) {
+          sa = sa + va[j].x; sb = sb + vb[j].x;
+          sa = sa + va[j].y; sb = sb + vb[j].y;
+          sa = sa + va[j].z; sb = sb + vb[j].z;
+          sa = sa + va[j].w; sb = sb + vb[j].w;
+        }
+      } else {
+        for (int j = 0; j < npa; j += 4) {
+          const float4 v = *(const float4 *)(pa + j);
+          sa = sa + v.x; sa = sa + v.y; sa = sa + v.z; sa = sa + v.w;
+        }
+        if (npb == CP) {
+          sb = chain_chunk<CP>(pb, sb);
+        } else {
+          for (int j = 0; j < npb; j += 4) {
+            const float4 v = *(const float4 *)(pb + j);
+            sb = sb + v.x; sb = sb + v.y; sb = sb + v.z; sb = sb + v.w;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && lane < T32) {
+    const int row = t * T32 + lane;
+    if (row < D.a.rows) {
+      const float attn = D.bias_a ? sa + D.bias_a[row] : sa;
+      const float ff = sb + D.bias_b[row];
+      D.inpL[row] = D.inpL[row] + (attn + ff);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64 * FW) k_gemv_fast_dual(DualJob D) {
+  __shared__ float part[2][FW * 2][T32];
+  const int t = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & (T32 - 1), h = lane >> 5;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const W4 &w = m == 0 ? D.a : D.b;
+    const uint8_t *xq = m == 0 ? D.xqa : D.xqb;
+    const float *xdd = m == 0 ? D.xdda : D.xddb;
+    const int nb = w.nb();
+    const uint8_t *qs = w.qs + (size_t)t * nb * T32 * 16;
+    const float *dd = w.d + (size_t)t * nb * T32;
+    float acc = 0.0f;
+    for (int b = 2 * wave + h; b < nb; b += 2 * FW) {
+      const size_t o = (size_t)b * T32 + r;
+      const uint4 q = *(const uint4 *)(qs + o * 16);
+      const float d0 = dd[o];
+      const uint4 xv = *(const uint4 *)(xq + (size_t)b * 16);
+      int sd = __builtin_amdgcn_sdot8((int)(q.x ^ 0x88888888u), (int)(xv.x ^ 0x88888888u), 0, false);
+      sd = __builtin_amdgcn_sdot8((int)(q.y ^ 0x88888888u), (int)(xv.y ^ 0x88888888u), sd, false);
+      sd = __builtin_amdgcn_sdot8((int)(q.z ^ 0x88888888u), (int)(xv.z ^ 0x88888888u), sd, false);
+      sd = __builtin_amdgcn_sdot8((int)(q.w ^ 0x88888888u), (int)(xv.w ^ 0x88888888u), sd, false);
+      acc = __builtin_fmaf(d0 * xdd[b], (float)sd, acc);
+    }
+    part[m][2 * wave + h][r] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < T32) {
+    float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2 * FW; ++i) {
+      sa += part[0][i][threadIdx.x];
+      sb += part[1][i][threadIdx.x];
+    }
+    const int row = t * T32 + threadIdx.x;
+    if (row < D.a.rows) {
+      const float attn = D.bias_a ? sa + D.bias_a[row] : sa;
+      const float ff = sb + D.bias_b[row];
+      D.inpL[row] = D.inpL[row] + (attn + ff);
+    }
+  }
+}
+
+int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s) {
+  if (D.a.rows != D.b.rows) { set_error("dual gemv: row mismatch"); return VSIM_EINVAL; }
+  if (mode == VSIM_MODE_EXACT)
+    hipLaunchKernelGGL((k_gemv_exact_dual<4, 7>), dim3(D.a.tiles), dim3(64 * 8), 0, s, D);
+  else
+    hipLaunchKernelGGL(k_gemv_fast_dual, dim3(D.a.tiles), dim3(64 * FW), 0, s, D);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// ------------------------------------------------------------------ 3. attention (N = 1)
+constexpr int ATT_THREADS = 256;
+
+__global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int h = blockIdx.x, d = A.d, E = A.d * A.H;
+  const int n_past = *A.npast;
+  const int nk = n_past + 1;
+  float *qh = sm;           // [d]
+  float *kh = sm + d;       // [d]
+  float *pr = sm + 2 * d;   // [nk] scores / probabilities
+  __shared__ float shf[ATT_THREADS / 64];
+  __shared__ double shd[ATT_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int i = tid; i < d; i += ATT_THREADS) {
+    qh[i] = A.q[h * d + i];
+    kh[i] = A.k[h * d + i];
+    A.vc[(size_t)n_past * E + h * d + i] = A.v[h * d + i];
+  }
+  __syncthreads();
+  // RoPE (ggml.c:6117-6152 / 5952-5973), position p = n_past for both q (mode 0) and k
+  const int half = A.n_rot / 2;
+  for (int j = tid; j < half; j += ATT_THREADS) {
+    const double2 c = A.cs[(size_t)n_past * half + j];
+    const int i0 = A.style == 0 ? j : 2 * j, i1 = A.style == 0 ? j + half : 2 * j + 1;
+    const double q0 = qh[i0], q1 = qh[i1], k0 = kh[i0], k1 = kh[i1];
+    if (A.style == 0) {
+      qh[i0] = (float)(c.x * q0 - c.y * q1);
+      qh[i1] = (float)(c.x * q1 + c.y * q0);
+      kh[i0] = (float)(c.x * k0 - c.y * k1);
+      kh[i1] = (float)(c.x * k1 + c.y * k0);
+    } else {
+      qh[i0] = (float)(q0 * c.x - q1 * c.y);
+      qh[i1] = (float)(q0 * c.y + q1 * c.x);
+      kh[i0] = (float)(k0 * c.x - k1 * c.y);
+      kh[i1] = (float)(k0 * c.y + k1 * c.x);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < d; i += ATT_THREADS) A.kc[(size_t)n_past * E + h * d + i] = kh[i];
+  // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale
+  float mx = -INFINITY;
+  for (int k = tid; k < nk; k += ATT_THREADS) {
+    const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
+    double acc = 0.0;
+    if (k == n_past) {
+      for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
+    } else {
+      for (int i = 0; i < d; i += 4) {
+        const float4 a = *(const float4 *)(kr + i);
+        acc += (double)(a.x * qh[i]);
+        acc += (double)(a.y * qh[i + 1]);
+        acc += (double)(a.z * qh[i + 2]);
+        acc += (double)(a.w * qh[i + 3]);
+      }
+    }
+    const float sc = (float)acc * A.scale;
+    pr[k] = sc;
+    mx = mx > sc ? mx : sc;
+  }
+  // max, exp via table, exact double sum (fp16 values: any order), 1/sum
+  mx = wave_max_f(mx);
+  if (lane == 0) shf[wid] = mx;
+  __syncthreads();
+  mx = shf[0];
+  for (int w = 1; w < ATT_THREADS / 64; ++w) mx = mx > shf[w] ? mx : shf[w];
+  double sum = 0.0;
+  for (int k = tid; k < nk; k += ATT_THREADS) {
+    const float val = h2f(A.etab[f2h(pr[k] - mx)]);
+    pr[k] = val;
+    sum += (double)val;
+  }
+  sum = wave_sum_d(sum);
+  if (lane == 0) shd[wid] = sum;
+  __syncthreads();
+  sum = (shd[0] + shd[1]) + (shd[2] + shd[3]);
+  const float inv = (float)(1.0 / sum);
+  for (int k = tid; k < nk; k += ATT_THREADS) pr[k] = pr[k] * inv;
+  __syncthreads();
+  // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f
+  for (int dd0 = 0; dd0 < d; dd0 += ATT_THREADS) {
+    const int dd = dd0 + tid;
+    float y = 0.0f;
+    if (dd < d) {
+      const float *vcol = A.vc + h * d + dd;
+      for (int k = 0; k < nk; ++k) y = y + vcol[(size_t)k * E] * pr[k];
+      if (A.out) A.out[h * d + dd] = y;
+    }
+    // quantize each 32-block of this head's output (wave-sized pieces of the d outputs)
+    const int blk = (h * d + dd0 + wid * 64) / QK;
+    if (dd0 + wid * 64 < d) {
+      quantize_block_lanes(y, lane, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
+      // lanes 32..63 of the wave hold the next block
+      const float y2 = __shfl_down(y, 32, 64);
+      if (dd0 + wid * 64 + 32 < d)
+        quantize_block_lanes(lane < 32 ? y2 : 0.0f, lane, A.oq_qs + (size_t)(blk + 1) * 16, A.oq_d + blk + 1,
+                             A.oxd + (size_t)(blk + 1) * QK);
+    }
+  }
+}
+
+int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s) {
+  if (A.d % 32 != 0) { set_error("attention: head dim must be a multiple of 32"); return VSIM_EINVAL; }
+  const size_t smem = (size_t)(2 * A.d + n_ctx) * sizeof(float);
+  hipLaunchKernelGGL(k_attn_decode, dim3(A.H), dim3(ATT_THREADS), smem, s, A);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+}  // namespace vsim

@@ -71,6 +71,15 @@ struct vsim_model {
   float *logit_host = nullptr;  // pinned
   int kernels_last = 0;
 
+  // fused single-token decode step (layer.hip) and its hipGraph
+  uint8_t *xqa = nullptr;     // attention output, quantized
+  float *xda = nullptr;
+  int *npast_dev = nullptr, *npast_host = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int graph_mode = -1;
+  int graph_kernels = 0;
+
   // GEMV profiling (bench.py's live roofline): event pair around every GEMV launch
   bool profile = false;
   std::vector<hipEvent_t> prof_events;
@@ -90,6 +99,18 @@ void free_scratch(vsim_model *m) {
     if (p) (void)hipFree(p);
   if (m->tok_host) (void)hipHostFree(m->tok_host);
   if (m->logit_host) (void)hipHostFree(m->logit_host);
+  if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
+  if (m->graph) (void)hipGraphDestroy(m->graph);
+  if (m->xqa) (void)hipFree(m->xqa);
+  if (m->xda) (void)hipFree(m->xda);
+  if (m->npast_dev) (void)hipFree(m->npast_dev);
+  if (m->npast_host) (void)hipHostFree(m->npast_host);
+  m->gexec = nullptr;
+  m->graph = nullptr;
+  m->graph_mode = -1;
+  m->xqa = nullptr;
+  m->xda = nullptr;
+  m->npast_dev = m->npast_host = nullptr;
   m->inpL = m->cur1 = m->cur2 = m->Qb = m->Kb = m->Vb = m->attn_in = m->attn = m->ff = m->fch = m->kq = m->logits =
       nullptr;
   m->xq1 = m->xq2 = m->xq3 = nullptr;
@@ -129,6 +150,10 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMalloc((void **)&m->tok_dev, n * sizeof(int32_t)));
   VSIM_HIP(hipHostMalloc((void **)&m->tok_host, n * sizeof(int32_t), hipHostMallocDefault));
   VSIM_HIP(hipHostMalloc((void **)&m->logit_host, V * sizeof(float), hipHostMallocDefault));
+  VSIM_HIP(ba(&m->xqa, E));
+  VSIM_HIP(fa(&m->xda, n * E));
+  VSIM_HIP(hipMalloc((void **)&m->npast_dev, sizeof(int)));
+  VSIM_HIP(hipHostMalloc((void **)&m->npast_host, sizeof(int), hipHostMallocDefault));
   m->n_max = n;
   return VSIM_OK;
 }
@@ -330,6 +355,145 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk));
   RC(launch_add_residual(m->inpL, m->attn, m->ff, N * E, (!gptj && !m->hp.use_parallel_residual) ? 1 : 0, s)); ++nk;
   return VSIM_OK;
+}
+
+// GEMV profiling brackets (eager launches only; bench.py's live roofline)
+hipEvent_t *prof_begin(vsim_model *m) {
+  if (!m->profile) return nullptr;
+  if (m->prof_used + 2 > m->prof_events.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return nullptr;
+    m->prof_events.push_back(a);
+    m->prof_events.push_back(b);
+  }
+  hipEvent_t *ev = &m->prof_events[m->prof_used];
+  m->prof_used += 2;
+  (void)hipEventRecord(ev[0], m->stream);
+  return ev;
+}
+void prof_end(vsim_model *m, hipEvent_t *ev, double bytes) {
+  if (!ev) return;
+  (void)hipEventRecord(ev[1], m->stream);
+  m->prof_bytes += bytes;
+}
+
+double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
+
+// The single-token decode step as 4 fused launches per layer (layer.hip).  Reads the token
+// from tok_dev and n_past from npast_dev, so the enqueued sequence is replayable.
+int enqueue_decode(vsim_model *m, int &nk) {
+  const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
+  const bool gptj = m->arch == VSIM_ARCH_GPTJ;
+  hipStream_t s = m->stream;
+  DevTables tab;
+  RC(tables_get(&tab));
+  const int nbE = E / QK, nbF = F / QK;
+  uint8_t *q1 = m->xq1, *q2 = m->xq2, *q3 = m->xq3, *qa = m->xqa;
+  float *d1 = (float *)(q1 + (size_t)nbE * 16), *d2 = (float *)(q2 + (size_t)nbE * 16);
+  float *d3 = (float *)(q3 + (size_t)nbF * 16), *da = (float *)(qa + (size_t)nbE * 16);
+  if (m->first) {
+    RC(launch_get_rows(m->wte, E, V, m->tok_dev, 1, m->inpL, s));
+    ++nk;
+  }
+  const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  for (int il = m->l0; il < m->l1; ++il) {
+    const LayerW &L = m->layers[il - m->l0];
+    const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
+    // 1. input LayerNorm (+ post_attention LayerNorm for GPT-NeoX), quantized
+    const LnQuantJob j1{m->inpL, L.ln1_w, L.ln1_b, q1, d1, m->xd1};
+    const LnQuantJob j2{m->inpL, L.ln2_w, L.ln2_b, q2, d2, m->xd2};
+    RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
+    ++nk;
+    // 2. {fc_in (+bias, GELU, requantize), Q, K, V (+bias)}
+    GemvBatch B{};
+    B.nj = 4;
+    auto job = [&](int i, void *W, int M, int K, const float *xd, const uint8_t *xq, const float *xdd,
+                   const float *bias, float *y) {
+      GemvJob &J = B.j[i];
+      J.w = w4_view(W, M, K);
+      J.xd = xd;
+      J.xqs = xq;
+      J.xdd = xdd;
+      J.bias = bias;
+      J.y = y;
+      J.epi = EPI_STORE;
+    };
+    job(0, L.wfc, F, E, gptj ? m->xd1 : m->xd2, gptj ? q1 : q2, gptj ? d1 : d2, L.bfc, nullptr);
+    B.j[0].epi = EPI_GELU_Q;
+    B.j[0].gelu_tab = tab.gelu_f16;
+    B.j[0].oq_qs = q3;
+    B.j[0].oq_d = d3;
+    B.j[0].oxd = m->xd3;
+    job(1, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
+    job(2, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
+    job(3, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
+    hipEvent_t *ev = prof_begin(m);
+    RC(launch_gemv_epi(B, m->mode, s));
+    prof_end(m, ev, w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
+    ++nk;
+    // 3. attention for the new token
+    AttnJob A{};
+    A.q = m->Qb;
+    A.k = m->Kb;
+    A.v = m->Vb;
+    A.kc = m->kcache + loff;
+    A.vc = m->vcache + loff;
+    A.npast = m->npast_dev;
+    A.cs = m->rope_cs;
+    A.etab = tab.exp_f16;
+    A.d = d;
+    A.H = H;
+    A.n_rot = m->hp.n_rot;
+    A.style = gptj ? 1 : 0;
+    A.scale = scale;
+    A.oq_qs = qa;
+    A.oq_d = da;
+    A.oxd = m->xda;
+    A.out = nullptr;
+    RC(launch_attn_decode(A, m->n_ctx, s));
+    ++nk;
+    // 4. out-projection + fc_out + residual
+    DualJob D{};
+    D.a = w4_view(L.wo, E, E);
+    D.b = w4_view(L.wproj, E, F);
+    D.xda = m->xda;
+    D.xdb = m->xd3;
+    D.xqa = qa;
+    D.xqb = q3;
+    D.xdda = da;
+    D.xddb = d3;
+    D.bias_a = gptj ? nullptr : L.bo;
+    D.bias_b = L.bproj;
+    D.inpL = m->inpL;
+    ev = prof_begin(m);
+    RC(launch_gemv_dual(D, m->mode, s));
+    prof_end(m, ev, w4_algo_bytes(D.a) + w4_algo_bytes(D.b));
+    ++nk;
+  }
+  if (m->last) {
+    const LnQuantJob jf{m->inpL, m->lnf_w, m->lnf_b, q1, d1, m->xd1};
+    RC(launch_ln_quant(jf, nullptr, E, s));
+    ++nk;
+    GemvBatch B{};
+    B.nj = 1;
+    B.j[0].w = w4_view(m->lmh, V, E);
+    B.j[0].xd = m->xd1;
+    B.j[0].xqs = q1;
+    B.j[0].xdd = d1;
+    B.j[0].bias = gptj ? m->lmh_b : nullptr;
+    B.j[0].y = m->logits;
+    B.j[0].epi = EPI_STORE;
+    hipEvent_t *ev = prof_begin(m);
+    RC(launch_gemv_epi(B, m->mode, s));
+    prof_end(m, ev, w4_algo_bytes(B.j[0].w));
+    ++nk;
+  }
+  return VSIM_OK;
+}
+
+bool fused_ok(const vsim_model *m, int N) {
+  static const bool disabled = getenv("VSIM_NO_FUSED") != nullptr;
+  return !disabled && N == 1 && (m->arch == VSIM_ARCH_GPTJ || m->hp.use_parallel_residual == 1);
 }
 
 thread_local std::string t_err;
@@ -566,30 +730,76 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
   const int E = m->hp.n_embd, V = m->hp.n_vocab;
   hipStream_t s = m->stream;
   int nk = 0;
-  if (m->first) {
-    if (!tokens) { set_error("eval: first stage needs tokens"); return VSIM_EINVAL; }
-    for (int i = 0; i < N; ++i) {
-      if (tokens[i] < 0 || tokens[i] >= V) { set_error("eval: token id out of range"); return VSIM_EINVAL; }
-      m->tok_host[i] = tokens[i];
+  if (fused_ok(m, N)) {
+    if (m->first) {
+      if (!tokens) { set_error("eval: first stage needs tokens"); return VSIM_EINVAL; }
+      if (tokens[0] < 0 || tokens[0] >= V) { set_error("eval: token id out of range"); return VSIM_EINVAL; }
+      m->tok_host[0] = tokens[0];
+      VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    } else {
+      if (!resid_in) { set_error("eval: non-first stage needs resid_in"); return VSIM_EINVAL; }
+      VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
     }
-    VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, N * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    RC(launch_get_rows(m->wte, E, V, m->tok_dev, N, m->inpL, s)); ++nk;
+    m->npast_host[0] = n_past;
+    VSIM_HIP(hipMemcpyAsync(m->npast_dev, m->npast_host, sizeof(int), hipMemcpyHostToDevice, s));
+    const bool use_graph = m->graph_enabled && m->first && m->last && !m->profile;
+    if (use_graph) {
+      if (!m->gexec || m->graph_mode != m->mode) {
+        if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
+        if (m->graph) (void)hipGraphDestroy(m->graph);
+        m->gexec = nullptr;
+        m->graph = nullptr;
+        VSIM_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        int gk = 0;
+        int rc = enqueue_decode(m, gk);
+        if (rc == 0 && hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s) !=
+                           hipSuccess)
+          rc = hip_fail(hipErrorUnknown, "capture logits copy");
+        hipGraph_t g = nullptr;
+        const hipError_t ce = hipStreamEndCapture(s, &g);
+        if (rc) return rc;
+        if (ce != hipSuccess) return hip_fail(ce, "hipStreamEndCapture");
+        m->graph = g;
+        VSIM_HIP(hipGraphInstantiate(&m->gexec, m->graph, nullptr, nullptr, 0));
+        m->graph_mode = m->mode;
+        m->graph_kernels = gk;
+      }
+      VSIM_HIP(hipGraphLaunch(m->gexec, s));
+      nk = m->graph_kernels;
+    } else {
+      RC(enqueue_decode(m, nk));
+      if (m->last && logits)
+        VSIM_HIP(hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s));
+      else if (!m->last && resid_out)
+        VSIM_HIP(hipMemcpyAsync(resid_out, m->inpL, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+    }
   } else {
-    if (!resid_in) { set_error("eval: non-first stage needs resid_in"); return VSIM_EINVAL; }
-    VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
-  }
-  for (int il = m->l0; il < m->l1; ++il) RC(run_layer(m, il, n_past, N, nk));
-  if (m->last) {
-    // only the last row's logits leave the eval (vsim.cpp:736-737); rows are independent
-    const float *xl = m->inpL + (size_t)(N - 1) * E;
-    RC(launch_norm(xl, m->cur1, E, 1, m->lnf_w, m->lnf_b, s)); ++nk;
-    RC(mm(m, m->lmh, V, E, m->cur1, 1, m->xq1, m->xd1, true, m->arch == VSIM_ARCH_GPTJ ? m->lmh_b : nullptr,
-          m->logits, nk));
-    if (logits) {
-      VSIM_HIP(hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s));
+    // general path: prompt batches (N > 1) and the serial-residual GPT-NeoX variant
+    if (m->first) {
+      if (!tokens) { set_error("eval: first stage needs tokens"); return VSIM_EINVAL; }
+      for (int i = 0; i < N; ++i) {
+        if (tokens[i] < 0 || tokens[i] >= V) { set_error("eval: token id out of range"); return VSIM_EINVAL; }
+        m->tok_host[i] = tokens[i];
+      }
+      VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, N * sizeof(int32_t), hipMemcpyHostToDevice, s));
+      RC(launch_get_rows(m->wte, E, V, m->tok_dev, N, m->inpL, s));
+      ++nk;
+    } else {
+      if (!resid_in) { set_error("eval: non-first stage needs resid_in"); return VSIM_EINVAL; }
+      VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
     }
-  } else if (resid_out) {
-    VSIM_HIP(hipMemcpyAsync(resid_out, m->inpL, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+    for (int il = m->l0; il < m->l1; ++il) RC(run_layer(m, il, n_past, N, nk));
+    if (m->last) {
+      // only the last row's logits leave the eval (vsim.cpp:736-737); rows are independent
+      const float *xl = m->inpL + (size_t)(N - 1) * E;
+      RC(launch_norm(xl, m->cur1, E, 1, m->lnf_w, m->lnf_b, s));
+      ++nk;
+      RC(mm(m, m->lmh, V, E, m->cur1, 1, m->xq1, m->xd1, true, m->arch == VSIM_ARCH_GPTJ ? m->lmh_b : nullptr,
+            m->logits, nk));
+      if (logits) VSIM_HIP(hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s));
+    } else if (resid_out) {
+      VSIM_HIP(hipMemcpyAsync(resid_out, m->inpL, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+    }
   }
   VSIM_HIP(hipStreamSynchronize(s));
   if (m->last && logits) memcpy(logits, m->logit_host, sizeof(float) * V);

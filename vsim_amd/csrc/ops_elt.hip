@@ -8,7 +8,7 @@
 #include <mutex>
 #include <vector>
 
-#include "common.hpp"
+#include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
 namespace vsim {
@@ -22,108 +22,16 @@ namespace vsim {
 //    (2n+64)*2^-53*sum(w); if both ends of that interval give the same float scale
 //    (the map S -> (float)(1/sqrt(S/n+eps)) is monotone) the scale is the reference's.
 // `stats` (optional) counts fallbacks: [0] mean, [1] variance.
-constexpr int NORM_THREADS = 256;
-
-__device__ __forceinline__ int ulp_exp(float x) {
-  const uint32_t b = __float_as_uint(x) & 0x7FFFFFFFu;
-  if (b == 0) return 1 << 30;
-  const int e = (int)(b >> 23);
-  return e == 0 ? -149 : e - 150;
-}
-
-template <typename T>
-__device__ T block_sum(T v, T *sh) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if (lane == 0) sh[wid] = v;
-  __syncthreads();
-  T r = 0;
-  for (int w = 0; w < NORM_THREADS / 64; ++w) r += sh[w];
-  return r;
-}
-
-__device__ int block_min(int v, int *sh) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  v = wave_min_i(v);
-  __syncthreads();
-  if (lane == 0) sh[wid] = v;
-  __syncthreads();
-  int r = sh[0];
-  for (int w = 1; w < NORM_THREADS / 64; ++w) r = min(r, sh[w]);
-  return r;
-}
-
 __global__ void __launch_bounds__(NORM_THREADS) k_norm_exact(const float *__restrict__ X, float *__restrict__ Y, int n,
                                                               const float *__restrict__ gw,
                                                               const float *__restrict__ gb, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float xrow[];
-  __shared__ double shd[NORM_THREADS / 64];
-  __shared__ int shi[NORM_THREADS / 64];
-  __shared__ double bcast_d;
-  __shared__ float bcast_f;
-  const float *x = X + (size_t)blockIdx.x * n;
+  ln_exact_lds(X + (size_t)blockIdx.x * n, xrow, n, gw, gb, stats);
   float *y = Y + (size_t)blockIdx.x * n;
-  const double eps = 1e-5f;
-
-  double s = 0.0, sa = 0.0;
-  int um = 1 << 30;
-  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    const float v = x[i];
-    xrow[i] = v;
-    s += (double)v;
-    sa += (double)fabsf(v);
-    um = min(um, ulp_exp(v));
-  }
-  s = block_sum(s, shd);
-  sa = block_sum(sa, shd);
-  um = block_min(um, shi);
-  const bool exact = (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
-  if (!exact) {
-    if (threadIdx.x == 0) {
-      double m = 0.0;
-      for (int i = 0; i < n; ++i) m += xrow[i];
-      bcast_d = m;
-      if (stats) atomicAdd(&stats[0], 1u);
-    }
-    __syncthreads();
-    s = bcast_d;
-  }
-  const double mean = s / n;
-
-  double s2 = 0.0;
-  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    const double v = (double)xrow[i] - mean;
-    s2 += v * v;
-  }
-  s2 = block_sum(s2, shd);
-  const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
-  const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
-  const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
-  float scale = sc_lo;
-  if (sc_lo != sc_hi) {
-    if (threadIdx.x == 0) {
-      double q = 0.0;
-      for (int i = 0; i < n; ++i) {
-        const double v = (double)xrow[i] - mean;
-        q += v * v;
-      }
-      bcast_f = (float)(1.0 / sqrt(q / n + eps));
-      if (stats) atomicAdd(&stats[1], 1u);
-    }
-    __syncthreads();
-    scale = bcast_f;
-  }
-  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    float v = (float)((double)xrow[i] - mean);
-    v = v * scale;
-    if (gw) v = (gw[i] * v) + gb[i];  // ggml_add(ggml_mul(repeat(w), cur), repeat(b))
-    y[i] = v;
-  }
+  for (int i = threadIdx.x; i < n; i += NORM_THREADS) y[i] = xrow[i];
 }
 
-static unsigned *g_norm_stats = nullptr;  // device counters, see vsim_norm_stats
+unsigned *g_norm_stats = nullptr;  // device counters of LayerNorm fallbacks (ln_exact_lds)
 
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s) {
   if (k <= 0 || rows <= 0) { set_error("norm: bad shape"); return VSIM_EINVAL; }

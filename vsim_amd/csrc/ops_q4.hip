@@ -10,7 +10,7 @@
 // tile the 16-byte nibble blocks are stored block-major, so the 32 rows' block b sit in
 // 512 contiguous bytes and the 32 scales of block b in 128 contiguous bytes.  A wave whose
 // lanes own rows reads whole cache lines; bytes per weight stay 0.625.
-#include "common.hpp"
+#include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
 namespace vsim {
@@ -104,36 +104,6 @@ int launch_act_unpack(const void *xq, void *aos, int n, int k, hipStream_t s) {
   return VSIM_OK;
 }
 
-// ------------------------------------------------------------------ activation quantize
-// One thread per 32-block.  Bit-identical to quantize_row_q4_0: fp32 amax, d = amax/7
-// (correctly rounded division), id = 1/d, q = (int8)round(x*id) + 8 with round-half-
-// away-from-zero, nibble pairs (q[2l], q[2l+1]).  Also emits xd = d*(q-8) per element,
-// the activation factor f2/f3 of the reference dot (ggml.c:497-498).
-__device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, float *d_out, float *xd_out) {
-  float amax = 0.0f;
-#pragma unroll
-  for (int l = 0; l < QK; ++l) amax = amax > fabsf(v[l]) ? amax : fabsf(v[l]);
-  const float d = amax / 7.0f;
-  const float id = d != 0.0f ? 1.0f / d : 0.0f;
-  uint32_t w[4] = {0, 0, 0, 0};
-  float out[QK];
-#pragma unroll
-  for (int l = 0; l < QK; l += 2) {
-    const int q0 = x86_round_i8(v[l] * id) + 8;
-    const int q1 = x86_round_i8(v[l + 1] * id) + 8;
-    w[l / 8] |= (uint32_t)((q0 & 0xF) | ((q1 & 0xF) << 4)) << (8 * ((l / 2) & 3));
-    out[l] = d * (float)(q0 - 8);
-    out[l + 1] = d * (float)(q1 - 8);
-  }
-  *(uint4 *)qs_out = make_uint4(w[0], w[1], w[2], w[3]);
-  *d_out = d;
-  if (xd_out) {
-    float4 *o = (float4 *)xd_out;
-#pragma unroll
-    for (int i = 0; i < QK / 4; ++i) o[i] = make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
-  }
-}
-
 __global__ void k_q4_quantize(const float *__restrict__ x, int k, int n, uint8_t *__restrict__ qs,
                               float *__restrict__ dd, float *__restrict__ xd) {
   const int nb = k / QK;
@@ -187,20 +157,6 @@ int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s) 
   return VSIM_OK;
 }
 
-// ------------------------------------------------------------------ pair products
-// The reference's per-byte term (imax.c:1219-1226): f0 = d0*(lo-8), f1 = d0*(hi-8),
-// p = f0*f2 + f1*f3, every product and the sum rounded separately (no FMA).  Nibbles of
-// four bytes are isolated with one AND and converted with v_cvt_f32_ubyteN.
-__device__ __forceinline__ void pair_terms4(uint32_t w, float d0, const float *x8, float *p4) {
-  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float f0 = d0 * ((float)((lo >> (8 * k)) & 0xFF) - 8.0f);
-    const float f1 = d0 * ((float)((hi >> (8 * k)) & 0xFF) - 8.0f);
-    p4[k] = f0 * x8[2 * k] + f1 * x8[2 * k + 1];
-  }
-}
-
 // ------------------------------------------------------------------ exact GEMV (N tokens)
 // One lane per (row, token) chain, reference order.  Used for prompt batches (N > 1).
 __global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__restrict__ xd, int n,
@@ -232,23 +188,8 @@ __global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__re
   y[(size_t)ic * W.rows + r] = bias ? acc + bias[r] : acc;
 }
 
-// Consumer step: add one full chunk of pairs into the chain.  All LDS reads are issued
-// before the first add (the hardware keeps up to 15 in flight), so the dependent add
-// chain does not stall on each read's latency.
-template <int CP>
-__device__ __forceinline__ float chain_chunk(const float *pr, float s) {
-  float4 v[CP / 4];
-#pragma unroll
-  for (int j = 0; j < CP / 4; ++j) v[j] = *(const float4 *)(pr + 4 * j);
-#pragma unroll
-  for (int j = 0; j < CP / 4; ++j) {
-    s = s + v[j].x;
-    s = s + v[j].y;
-    s = s + v[j].z;
-    s = s + v[j].w;
-  }
-  return s;
-}
+// ------------------------------------------------------------------ activation quantize
+// (quantize_block: kern.hpp)
 
 // ------------------------------------------------------------------ exact GEMV (decode)
 // Producer/consumer over one 32-row tile and the whole K (the chain order forbids
