@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__re
 // fill the other LDS slot.  Layout [slot][row][pair] with a 4-float pad: producer
 // ds_write_b128 (8-lane groups on distinct 4-bank groups) and consumer ds_read_b128
 // (16-lane groups covering all 64 banks) are conflict-free.
-template <int C, int NPW>
+template <int C, int NPW, int DBG = 0>  // DBG (diagnostics only): 1 = no global loads, 2 = no producers
 __global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_pc(GemvBatch B) {
   constexpr int CP = C * 16;  // pairs per row per chunk
   constexpr int LD = CP + 4;  // padded row stride (floats)
@@ -214,16 +214,16 @@ __global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_pc(GemvBatch B) {
   const float *dd = J.w.d + (size_t)t * nb * T32;
   float s = 0.0f;
   for (int c = 0; c <= nchunks; ++c) {
-    if (wave > 0 && c < nchunks) {
+    if (DBG != 2 && wave > 0 && c < nchunks) {
       float *Ps = P[c & 1];
       for (int i = (wave - 1) * 64 + lane; i < T32 * C; i += NPW * 64) {
         const int r = i & (T32 - 1), b = i / T32;
         const int blk = c * C + b;
         if (blk < nb) {
           const size_t o = (size_t)blk * T32 + r;
-          const float d0 = dd[o];
-          const uint4 q = *(const uint4 *)(qs + o * 16);
-          const float4 *xv = (const float4 *)(J.xd + (size_t)blk * QK);
+          const float d0 = DBG == 1 ? (float)o * 1e-6f : dd[o];
+          const uint4 q = DBG == 1 ? make_uint4(o, o * 3, o * 5, o * 7) : *(const uint4 *)(qs + o * 16);
+          const float4 *xv = (const float4 *)(J.xd + (size_t)(DBG == 1 ? 0 : blk) * QK);
           const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
           float4 *dst = (float4 *)(Ps + r * LD + b * 16);
 #pragma unroll
@@ -433,6 +433,9 @@ int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
       case 7: hipLaunchKernelGGL((k_gemv_exact_v2<2, 13>), dim3(tiles), dim3(64 * 14), 0, s, B); break;
       case 8: hipLaunchKernelGGL((k_gemv_exact_v2<8, 3>), dim3(tiles), dim3(64 * 4), 0, s, B); break;
       case 9: hipLaunchKernelGGL((k_gemv_exact_v2<2, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
+      case 10: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7, 1>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
+      case 11: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7, 2>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
+      case 12: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
       default: hipLaunchKernelGGL((k_gemv_exact_pc<8, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
     }
   } else {
