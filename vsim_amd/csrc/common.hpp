@@ -109,6 +109,8 @@ int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream
 int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s);
 int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s);
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s);
+// exact-mode chain GEMV (gemv_chain.hip): a batch of jobs with the GemvBatch epilogues
+int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s);
 
 // ---------------------------------------------------------------- fp16 (ggml.c:95-142)
 __device__ __forceinline__ float bits_f(uint32_t w) { return __uint_as_float(w); }

@@ -1,0 +1,362 @@
+// vsim_amd/csrc/gemv_chain.hip — exact-mode Q4_0 GEMV (decode, one activation row).
+//
+// The reference dot (imax.c:1182-1230 / ggml.c:1471-1500) is one sequential fp32 chain per
+// output row: sumf += f0*f2 + f1*f3 over the K/2 bytes of the row, every product and sum
+// rounded separately.  The chain cannot be re-associated without changing the result, so
+// the kernel is bounded by the dependent-add latency of the chain (≈7.8 cycles per add on
+// gfx950, one chain per lane), not by HBM: K = 16384 is 8192 dependent adds ≈ 27 µs.  Every
+// other cost is arranged to hide behind that chain.  One workgroup = 64 rows (two W4T32
+// tiles) of one job:
+//
+//  * the consumer wave runs the 64 chains, one per lane: a lane reads its row's pair terms
+//    from LDS (16-byte reads, a few ahead of the adds) and adds them in order;
+//  * CH_NPW producer waves compute the pair terms, one block of the chunk each: 16 pairs
+//    of one Q4_0 block for the 64 rows.  Nibbles and scales stream into an
+//    LDS ring by LDS-DMA (global_load_lds), CH_DEPTH chunks ahead, and are read into
+//    registers one chunk before use; the item's activation factors are wave-uniform and
+//    come into SGPRs by scalar loads one chunk ahead.
+//    Two producer waves share each SIMD (one wave alone issues VALU at ≈5 cycles per
+//    instruction; a second wave nearly doubles the SIMD's rate), and a 128-pair chunk
+//    amortizes the per-chunk barrier and wait latencies;
+//  * a 3-slot LDS ring of pair terms, one s_barrier per chunk: in iteration k producers
+//    fill chunk k while the consumer adds chunk k-2 (and reads ahead into chunk k-1).
+//
+// Epilogues: plain store (+bias), and fc_in's bias + GELU table + re-quantization of the
+// 64 outputs into two blocks of the next product's Q4_0 activation (ggml.c:5024-5041).
+#include <cstdlib>
+
+#include "kern.hpp"
+#include "../../include/vsim_hip.h"
+
+namespace vsim {
+
+constexpr int CH_CB = 8;                 // Q4_0 blocks per chunk
+constexpr int CH_CP = CH_CB * 16;        // pairs per row per chunk
+constexpr int CH_LD = CH_CP + 4;         // LDS row stride (floats): conflict-free b128 access
+constexpr int CH_NPW = CH_CB;            // producer waves: one per block of the chunk
+constexpr int CH_THREADS = 64 * (1 + CH_NPW);
+constexpr int CH_RING = 3;               // pair-term ring slots
+constexpr int CH_WIN = 8;                // consumer read-ahead (16-byte reads)
+constexpr int CH_DEPTH = 4;              // LDS-DMA prefetch depth (chunks)
+constexpr int CH_RAW = CH_DEPTH + 1;     // raw weight ring slots
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int WAIT_VM_DEPTH = 0x0F70 | (2 * (CH_DEPTH - 2));  // two DMA ops per chunk per wave
+
+static_assert(CH_DEPTH >= 3 && 2 * (CH_DEPTH - 2) < 16, "vmcnt immediate");
+
+typedef const __attribute__((address_space(4))) float sfloat;  // scalar-loaded
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
+
+// LDS-DMA: each lane's 16 (4) bytes from its own global address land lane-linearly at the
+// wave-uniform LDS address.  Inline asm keeps the load out of the compiler's wait-count
+// bookkeeping: completion is retired by the explicit vmcnt waits.  nt: streamed once.
+__device__ __forceinline__ void glds16(const void *g, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+
+struct ChainRows {
+  const uint8_t *qs0, *qs1;  // nibble planes of the two 32-row tiles (qs1 null: absent)
+  const float *d0, *d1;
+  const float *x;            // dequantized activation factors, K floats
+  int nb;                    // K/32
+  int job, g;                // batch job (-1: grid tail), 64-row group within it
+};
+
+// Field-wise reads of the kernel arguments with wave-uniform indices (whole-struct copies
+// make the compiler spill the argument block to private memory).
+__device__ __forceinline__ void chain_rows(const GemvBatch &B, ChainRows &S) {
+  S.nb = 0;
+  S.job = -1;
+  S.qs1 = nullptr;
+  S.d1 = nullptr;
+  int g = blockIdx.x, ji = 0;
+  while (ji < B.nj) {
+    const int ng = (B.j[ji].w.tiles + 1) / 2;
+    if (g < ng) break;
+    g -= ng;
+    ++ji;
+  }
+  if (ji >= B.nj) return;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const uint8_t *wqs = B.j[ji].w.qs;
+  const float *wd = B.j[ji].w.d;
+  const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK;
+  S.x = B.j[ji].xd;
+  S.job = ji;
+  S.nb = nb;
+  S.g = g;
+  S.qs0 = wqs + (size_t)(2 * g) * nb * T32 * 16;
+  S.d0 = wd + (size_t)(2 * g) * nb * T32;
+  if (2 * g + 1 < tiles) {
+    S.qs1 = wqs + (size_t)(2 * g + 1) * nb * T32 * 16;
+    S.d1 = wd + (size_t)(2 * g + 1) * nb * T32;
+  }
+}
+
+// Quantize one 32-value block per half-wave (lanes 0-31 -> block A, 32-63 -> block B) with
+// quantize_row_q4_0 semantics (see quantize_block_lanes in kern.hpp).
+__device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
+                                              float *xd_out) {
+  float a = fabsf(v);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    const float t = __shfl_xor(a, o, 64);
+    a = a > t ? a : t;
+  }
+  const float d = a / 7.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  const int q = x86_round_i8(v * id) + 8;
+  const int l = lane & 31;
+  const int qn = __shfl_xor(q, 1, 64);
+  const uint32_t byte = (l & 1) ? 0u : (uint32_t)((q & 0xF) | ((qn & 0xF) << 4));
+  uint32_t word = byte << (8 * ((l >> 1) & 3));
+  word |= __shfl_xor(word, 2, 64);
+  word |= __shfl_xor(word, 4, 64);
+  if (ok) {
+    if ((l & 7) == 0) ((uint32_t *)qs_out)[l >> 3] = word;
+    if (l == 0) *d_out = d;
+    xd_out[l] = d * (float)(q - 8);
+  }
+}
+
+// timing experiment output (DBG & 8): [0..3] producer wave 0 of block 0, [4] iterations,
+// [8..9] consumer of block 0 (cycles summed over iterations)
+__device__ unsigned long long g_chain_prof[64];
+
+// DBG (timing experiments only; results are wrong unless 0 or 8): bit0 = the consumer skips
+// the adds, bit1 = producers skip the pair terms, bit2 = producers skip the LDS-DMA
+template <int DBG>
+__global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
+  __shared__ __attribute__((aligned(16))) float P[CH_RING][64 * CH_LD];
+  __shared__ __attribute__((aligned(16))) uint4 RQ[CH_RAW][CH_CB][64];
+  __shared__ __attribute__((aligned(16))) float RD[CH_RAW][CH_CB][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  ChainRows S;
+  chain_rows(B, S);
+  if (S.job < 0) return;  // whole workgroup: no barrier is reached
+  const int nb = S.nb, nch = (nb + CH_CB - 1) / CH_CB;
+  // iterations (one barrier each, after a prologue barrier): chunk k is produced in
+  // iteration k and added in k+2; even count for the producers' two x register sets
+  const int nit = (nch + 2 + 1) & ~1;
+
+  if (wave > 0) {
+    // ------------------------------------------------------------- producer
+    // Step k issues everything for later chunks first and then computes: scalar loads of
+    // the activation factors of chunk k+1, LDS reads of chunk k+1's raw block (landed before
+    // the previous barrier), LDS-DMA of chunk k+DEPTH; then chunk k's pair terms from the
+    // registers filled in step k-1 -> P; wait until this wave's DMA of chunk k+2 landed;
+    // barrier (its lgkmcnt(0) retires this step's reads).
+    const int p = wave - 1, o = p;
+    const int r = lane & 31, h = lane >> 5;
+    const bool tile_ok = h == 0 || S.qs1 != nullptr;
+    const uint8_t *qs = (tile_ok && h ? S.qs1 : S.qs0) + (size_t)r * 16;
+    const float *dd = (tile_ok && h ? S.d1 : S.d0) + r;
+    int dslot = 0;  // raw slot of chunk k+DEPTH (advanced per step)
+    auto dma = [&](int c, int slot) {  // chunk c, block clamped so every load stays in bounds
+      const int b = min(c * CH_CB + o, nb - 1);
+      glds16(qs + (size_t)b * (T32 * 16), lds_addr(&RQ[slot][o][0]));
+      glds4(dd + (size_t)b * T32, lds_addr(&RD[slot][o][0]));
+    };
+    auto ldx = [&](int c, f32x2 *xv) {  // this item's 32 activation factors (16 pairs)
+      const int b = min(c * CH_CB + o, nb - 1);
+      const sfloat *xp = (const sfloat *)(S.x + (size_t)b * QK);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        xv[i].x = xp[2 * i];
+        xv[i].y = xp[2 * i + 1];
+      }
+    };
+    int rslot = 0;  // raw slot of chunk k+1
+    auto ldraw = [&](int slot, uint4 &q, float &dq) {
+      q = RQ[slot][o][lane];
+      dq = RD[slot][o][lane];
+    };
+    const bool prof = (DBG & 8) && blockIdx.x == 0;
+    unsigned long long pt[4] = {0, 0, 0, 0}, tp = 0;
+    auto stamp = [&](int i) {
+      if (DBG & 8) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (i >= 0) pt[i] += t - tp;
+        tp = t;
+      }
+    };
+    int ps = 0;  // P ring slot of chunk k
+    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const uint4 &qc, float dqc, uint4 &qn, float &dqn) {
+      stamp(-1);
+      ldx(k + 1, xn);
+      rslot = rslot == CH_RAW - 1 ? 0 : rslot + 1;
+      ldraw(rslot, qn, dqn);
+      if (!(DBG & 4)) dma(k + CH_DEPTH, dslot);
+      dslot = dslot == CH_RAW - 1 ? 0 : dslot + 1;
+      __builtin_amdgcn_sched_barrier(0);
+      stamp(0);
+      if (!(DBG & 2)) {
+        const float dv = tile_ok && k * CH_CB + o < nb ? dqc : 0.0f;
+        const f32x2 d2 = {dv, dv}, m2 = {-8.0f * dv, -8.0f * dv};
+        float *dst = &P[ps][lane * CH_LD + o * 16];
+        const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) {
+          float p4[4];
+          pair_terms4_fma(qw[wv], d2, m2, xc + 4 * wv, p4);
+          *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+        }
+      }
+      ps = ps == CH_RING - 1 ? 0 : ps + 1;
+      stamp(1);
+      __builtin_amdgcn_s_waitcnt(WAIT_VM_DEPTH);  // this wave's DMA of chunk k+2 landed
+      stamp(2);
+      __syncthreads();
+      stamp(3);
+    };
+#pragma unroll
+    for (int c = 0; c < CH_DEPTH; ++c) dma(c, c);
+    dslot = CH_DEPTH % CH_RAW;
+    f32x2 xa[16], xb[16];
+    uint4 qa, qb;
+    float da, db;
+    ldx(0, xa);
+    __builtin_amdgcn_s_waitcnt(WAIT_VM_DEPTH);  // chunks 0 and 1 landed
+    __syncthreads();
+    ldraw(0, qa, da);
+    __syncthreads();  // (second prologue barrier: the reads above are retired here)
+    for (int k = 0; k < nit; k += 2) {
+      step(k, xa, xb, qa, da, qb, db);
+      step(k + 1, xb, xa, qb, db, qa, da);
+    }
+    if (prof && lane == 0) {
+      for (int i = 0; i < 4; ++i) g_chain_prof[16 + 4 * p + i] = pt[i];
+      if (p == 0) {
+        for (int i = 0; i < 4; ++i) g_chain_prof[i] = pt[i];
+        g_chain_prof[4] = nit;
+      }
+    }
+    return;
+  }
+
+  // --------------------------------------------------------------- consumer
+  // Rolling window of CH_WIN 16-byte LDS reads ahead of the chain (few registers, so two
+  // workgroups fit per CU): iteration k adds chunk k-2 and, near its end, reads the first
+  // window of chunk k-1 (published one barrier earlier; the 3-slot ring keeps both alive).
+  float acc = 0.0f;
+  float4 win[CH_WIN];
+  auto src = [&](int c) { return &P[c % CH_RING][lane * CH_LD]; };
+  __builtin_amdgcn_s_setprio(3);  // the chain issues first whenever it is ready
+  __syncthreads();  // prologue (producers: chunks 0 and 1 landed)
+  __syncthreads();  // prologue (producers: raw chunk 0 in registers)
+  unsigned long long ct[2] = {0, 0}, tc = 0;
+  auto cstamp = [&](int i) {
+    if (DBG & 8) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (i >= 0) ct[i] += t - tc;
+      tc = t;
+    }
+  };
+  for (int k = 0; k < nit; ++k) {
+    cstamp(-1);
+    const int c = k - 2;
+    if (c == -1 && nch > 0) {
+      const float *p0 = src(0);
+#pragma unroll
+      for (int j = 0; j < CH_WIN; ++j) win[j] = *(const float4 *)(p0 + 4 * j);
+    } else if (c >= 0 && c < nch) {
+      // groups pinned in order (4 adds, then the next read) so the scheduler cannot hoist the
+      // reads into one burst with a full wait in front of the adds; the reads past the
+      // chunk's end come from chunk c+1's slot (stale when c+1 == nch, never added)
+      const float *pc = src(c), *pn = src(c + 1);
+#pragma unroll
+      for (int j = 0; j < CH_CP / 4; ++j) {
+        const float4 v = win[j % CH_WIN];
+        if (!(DBG & 1)) {
+          acc = acc + v.x;
+          acc = acc + v.y;
+          acc = acc + v.z;
+          acc = acc + v.w;
+        }
+        const int jn = j + CH_WIN;
+        win[j % CH_WIN] = jn < CH_CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - CH_CP / 4));
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read x1
+      }
+    }
+    cstamp(0);
+    __syncthreads();
+    cstamp(1);
+  }
+  if ((DBG & 8) && blockIdx.x == 0 && lane == 0) {
+    g_chain_prof[8] = ct[0];
+    g_chain_prof[9] = ct[1];
+  }
+
+  // ----------------------------------------------------------------- epilogue
+  const int ji = S.job;
+  const int row = S.g * 64 + lane;
+  const int rows = B.j[ji].w.rows;
+  const float *bias = B.j[ji].bias;
+  float *y = B.j[ji].y;
+  if (B.j[ji].epi == EPI_GELU_Q) {
+    const bool ok = row < rows;
+    float g = 0.0f;
+    if (ok) {
+      g = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      if (y) y[row] = g;
+    }
+    const int blk = row / QK;
+    quantize_half(g, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
+                  B.j[ji].oxd + (size_t)blk * QK);
+  } else if (row < rows) {
+    y[row] = bias ? acc + bias[row] : acc;
+  }
+}
+
+template <int DBG>
+static void chain_launch_t(int grid, const GemvBatch &B, hipStream_t s) {
+  hipLaunchKernelGGL(k_gemv_chain<DBG>, dim3(grid), dim3(CH_THREADS), 0, s, B);
+}
+
+int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
+  int groups = 0;
+  for (int i = 0; i < B.nj; ++i) {
+    if (B.j[i].w.k % QK != 0 || B.j[i].w.k <= 0) {
+      set_error("gemv: K must be a positive multiple of 32");
+      return VSIM_EINVAL;
+    }
+    if (!B.j[i].xd) { set_error("gemv: exact mode needs the activation factors xd"); return VSIM_EINVAL; }
+    groups += (B.j[i].w.tiles + 1) / 2;
+  }
+  if (groups == 0) return VSIM_OK;
+  static const int dbg = [] {
+    const char *e = getenv("VSIM_CHAIN_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  switch (dbg) {
+    case 1: chain_launch_t<1>(groups, B, s); break;
+    case 2: chain_launch_t<2>(groups, B, s); break;
+    case 3: chain_launch_t<3>(groups, B, s); break;
+    case 4: chain_launch_t<4>(groups, B, s); break;
+    case 5: chain_launch_t<5>(groups, B, s); break;
+    case 7: chain_launch_t<7>(groups, B, s); break;
+    case 12: chain_launch_t<12>(groups, B, s); break;
+    case 8: chain_launch_t<8>(groups, B, s); break;
+    default: chain_launch_t<0>(groups, B, s); break;
+  }
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+}  // namespace vsim
+
+// timing-experiment readout (tools/gemv_bench.py); not part of include/vsim_hip.h
+extern "C" int vsim_debug_chain_prof(unsigned long long *out64) {
+  return hipMemcpyFromSymbol(out64, HIP_SYMBOL(vsim::g_chain_prof), 64 * sizeof(unsigned long long)) == hipSuccess
+             ? 0 : -1;
+}

@@ -1,6 +1,8 @@
 // vsim_amd/csrc/kern.hpp — device building blocks shared by the kernel files.
 #pragma once
 
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace vsim {
@@ -37,16 +39,69 @@ __device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, 
 
 // ------------------------------------------------------------------ pair products
 // The reference's per-byte term (imax.c:1219-1226): f0 = d0*(lo-8), f1 = d0*(hi-8),
-// p = f0*f2 + f1*f3, every product and the sum rounded separately (no FMA).  Nibbles of
-// four bytes are isolated with one AND and converted with v_cvt_f32_ubyteN.
+// p = f0*f2 + f1*f3, every product and the sum rounded separately (no FMA).  The nibble
+// value n - 8 is formed exactly as (2^23 + n) - (2^23 + 8): v_perm_b32 places nibble byte k
+// under the exponent byte 0x4B, and the subtraction pairs up into v_pk_add_f32.
 __device__ __forceinline__ void pair_terms4(uint32_t w, float d0, const float *x8, float *p4) {
   const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float f0 = d0 * ((float)((lo >> (8 * k)) & 0xFF) - 8.0f);
-    const float f1 = d0 * ((float)((hi >> (8 * k)) & 0xFF) - 8.0f);
+    const float n0 = __uint_as_float(__builtin_amdgcn_perm(0x4B4B4B4Bu, lo, 0x040C0C00u | k)) - 8388616.0f;
+    const float n1 = __uint_as_float(__builtin_amdgcn_perm(0x4B4B4B4Bu, hi, 0x040C0C00u | k)) - 8388616.0f;
+    const float f0 = d0 * n0, f1 = d0 * n1;
     p4[k] = f0 * x8[2 * k] + f1 * x8[2 * k + 1];
   }
+}
+
+// The same terms with each pair's two products packed together, {f0, f1} * {x[2k], x[2k+1]}:
+// the activation factors are used as adjacent (SGPR) pairs, no operand shuffles.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pair_terms4_pk(uint32_t w, float d0, const f32x2 *x4, float *p4) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f32x2 n;
+    n.x = __uint_as_float(__builtin_amdgcn_perm(0x4B4B4B4Bu, lo, 0x040C0C00u | k));
+    n.y = __uint_as_float(__builtin_amdgcn_perm(0x4B4B4B4Bu, hi, 0x040C0C00u | k));
+    n = n - 8388616.0f;
+    const f32x2 f = d0 * n;
+    const f32x2 t = f * x4[k];
+    p4[k] = t.x + t.y;
+  }
+}
+
+// v_cvt_f32_ubyteK: byte K of a word as float, one instruction (left to itself the compiler
+// extracts each byte first)
+template <int K>
+__device__ __forceinline__ float cvt_ubyte(uint32_t w) {
+  float f;
+  if (K == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(w));
+  if (K == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(w));
+  if (K == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(w));
+  if (K == 3) asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(w));
+  return f;
+}
+
+// The same terms with f = d0*(n-8) as one fused multiply-add: fma(n, d0, -8*d0) rounds the
+// exact product d0*(n-8) once, as the reference's d0*(float)(n-8) does (-8*d0 is exact, n
+// exact), for every finite d0.  n comes from v_cvt_f32_ubyteN on the masked nibble bytes.
+// Zero signs of a term may differ from the reference (0*(n-8) vs fma's +0); a chain that
+// starts at +0 is unaffected by the sign of a zero term.
+__device__ __forceinline__ void pair_terms4_fma(uint32_t w, f32x2 d2, f32x2 m2, const f32x2 *x4, float *p4) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+  auto term = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    f32x2 n;
+    n.x = cvt_ubyte<k>(lo);
+    n.y = cvt_ubyte<k>(hi);
+    const f32x2 f = __builtin_elementwise_fma(n, d2, m2);
+    const f32x2 t = f * x4[k];
+    p4[k] = t.x + t.y;
+  };
+  term(std::integral_constant<int, 0>{});
+  term(std::integral_constant<int, 1>{});
+  term(std::integral_constant<int, 2>{});
+  term(std::integral_constant<int, 3>{});
 }
 
 // Consumer step: add one full chunk of pairs into the chain.  All LDS reads are issued

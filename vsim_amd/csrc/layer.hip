@@ -14,6 +14,8 @@
 // Every value is computed with the reference's operation order and rounding (exact mode);
 // the fast mode swaps in the integer-dot GEMV bodies.  n_past is read from device memory so
 // the whole step can be captured once in a hipGraph and replayed per token.
+#include <cstdlib>
+
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
@@ -156,9 +158,15 @@ __global__ void __launch_bounds__(64 * FW) k_gemv_fast_epi(GemvBatch B) {
   }
 }
 
+static bool legacy_exact() {
+  static const bool v = getenv("VSIM_LEGACY_EXACT") != nullptr;
+  return v;
+}
+
 int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s) {
   int tiles = 0;
   for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
+  if (mode == VSIM_MODE_EXACT && !legacy_exact()) return launch_gemv_chain_batch(B, s);
   if (mode == VSIM_MODE_EXACT)
     hipLaunchKernelGGL((k_gemv_exact_epi<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B);
   else

@@ -423,7 +423,8 @@ int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
       const char *e = getenv("VSIM_GEMV_PC");
       return e ? atoi(e) : 0;
     }();
-    switch (variant) {  // tuning knob: chunk blocks C x producer waves NPW
+    if (variant == 0) return launch_gemv_chain_batch(B, s);  // gemv_chain.hip
+    switch (variant) {  // older producer/consumer kernels kept for A/B timing
       case 1: hipLaunchKernelGGL((k_gemv_exact_pc<4, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
       case 2: hipLaunchKernelGGL((k_gemv_exact_pc<16, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
       case 3: hipLaunchKernelGGL((k_gemv_exact_pc<8, 3>), dim3(tiles), dim3(64 * 4), 0, s, B); break;
