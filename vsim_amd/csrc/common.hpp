@@ -79,6 +79,10 @@ struct LnQuantJob {
   uint8_t *qs;         // [n/32][16]
   float *d;            // [n/32]
   float *xd;           // [n]
+  // optional residual join of the previous layer before the norm (ja == null: none):
+  // row = x + ((ja + jab) + (jf + jfb)), stored to jout when non-null
+  const float *ja, *jab, *jf, *jfb;
+  float *jout;
 };
 
 // Rows [32t, 32t+32) of the out-projection (a) and of fc_out (b) in one workgroup, epilogue
@@ -106,6 +110,9 @@ struct AttnJob {
 };
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s);
+// out[i] = x[i] + ((a[i] + ab[i]) + (f[i] + fb[i]))  (ab may be null): the residual join alone
+int launch_residual_join(const float *x, const float *a, const float *ab, const float *f, const float *fb, float *out,
+                         int n, hipStream_t s);
 int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s);
 int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s);
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s);

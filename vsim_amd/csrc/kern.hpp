@@ -172,8 +172,15 @@ namespace vsim {
 //    (the map S -> (float)(1/sqrt(S/n+eps)) is monotone) the scale is the reference's.
 // Optional affine y = w*y + b (ggml_add(ggml_mul(repeat(w), cur), repeat(b))).
 // stats (optional): [0] mean fallbacks, [1] variance fallbacks.
+// Optional residual join first (the previous layer's, vsim.cpp:694-695): the normalized row is
+// v = x + ((ja + jab) + (jf + jfb)) (jab may be null), written to jout when jout != null.
+struct LnJoin {
+  const float *ja, *jab, *jf, *jfb;
+  float *jout;
+};
+
 __device__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
-                             const float *__restrict__ gb, unsigned *stats) {
+                             const float *__restrict__ gb, unsigned *stats, const LnJoin *J = nullptr) {
   __shared__ double shd[NORM_THREADS / 64];
   __shared__ int shi[NORM_THREADS / 64];
   __shared__ double bcast_d;
@@ -182,7 +189,13 @@ __device__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, con
   double s = 0.0, sa = 0.0;
   int um = 1 << 30;
   for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    const float v = x[i];
+    float v = x[i];
+    if (J) {
+      const float attn = J->jab ? J->ja[i] + J->jab[i] : J->ja[i];
+      const float ff = J->jf[i] + J->jfb[i];
+      v = v + (attn + ff);
+      if (J->jout) J->jout[i] = v;
+    }
     row[i] = v;
     s += (double)v;
     sa += (double)fabsf(v);

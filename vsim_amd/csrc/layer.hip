@@ -27,7 +27,8 @@ extern unsigned *g_norm_stats;
 __global__ void __launch_bounds__(NORM_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float row[];
   const LnQuantJob J = blockIdx.x == 0 ? j0 : j1;
-  ln_exact_lds(J.x, row, n, J.w, J.b, stats);
+  const LnJoin jn{J.ja, J.jab, J.jf, J.jfb, J.jout};
+  ln_exact_lds(J.x, row, n, J.w, J.b, stats, J.ja ? &jn : nullptr);
   const int nb = n / QK;
   for (int b = threadIdx.x; b < nb; b += NORM_THREADS) {
     float v[QK];
@@ -40,6 +41,21 @@ __global__ void __launch_bounds__(NORM_THREADS) k_ln_quant(LnQuantJob j0, LnQuan
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_ln_quant, dim3(j1 ? 2 : 1), dim3(NORM_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
                      g_norm_stats);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+__global__ void k_residual_join(const float *x, const float *a, const float *ab, const float *f, const float *fb,
+                                float *out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float attn = ab ? a[i] + ab[i] : a[i];
+  out[i] = x[i] + (attn + (f[i] + fb[i]));
+}
+
+int launch_residual_join(const float *x, const float *a, const float *ab, const float *f, const float *fb, float *out,
+                         int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_residual_join, dim3((n + 255) / 256), dim3(256), 0, s, x, a, ab, f, fb, out, n);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

@@ -74,6 +74,8 @@ struct vsim_model {
   // fused single-token decode step (layer.hip) and its hipGraph
   uint8_t *xqa = nullptr;     // attention output, quantized
   float *xda = nullptr;
+  float *inpL2 = nullptr;     // second residual buffer (the join alternates between the two)
+  float *resid_final = nullptr;  // where the last fused step left the stage's residual
   int *npast_dev = nullptr, *npast_host = nullptr;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
@@ -103,6 +105,8 @@ void free_scratch(vsim_model *m) {
   if (m->graph) (void)hipGraphDestroy(m->graph);
   if (m->xqa) (void)hipFree(m->xqa);
   if (m->xda) (void)hipFree(m->xda);
+  if (m->inpL2) (void)hipFree(m->inpL2);
+  m->inpL2 = nullptr;
   if (m->npast_dev) (void)hipFree(m->npast_dev);
   if (m->npast_host) (void)hipHostFree(m->npast_host);
   m->gexec = nullptr;
@@ -152,6 +156,7 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipHostMalloc((void **)&m->logit_host, V * sizeof(float), hipHostMallocDefault));
   VSIM_HIP(ba(&m->xqa, E));
   VSIM_HIP(fa(&m->xda, n * E));
+  VSIM_HIP(fa(&m->inpL2, E));
   VSIM_HIP(hipMalloc((void **)&m->npast_dev, sizeof(int)));
   VSIM_HIP(hipHostMalloc((void **)&m->npast_host, sizeof(int), hipHostMallocDefault));
   m->n_max = n;
@@ -396,20 +401,40 @@ int enqueue_decode(vsim_model *m, int &nk) {
     ++nk;
   }
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  // The residual join of layer l (inpL += attn + ff, vsim.cpp:694-695) runs inside layer
+  // l+1's LayerNorm kernel (or the final norm); the joined row goes to the other of the two
+  // residual buffers, so both norm workgroups of GPT-NeoX can read the old one.
+  float *R[2] = {m->inpL, m->inpL2};
+  int cur = 0;
+  bool pending = false;
+  const float *pend_ab = nullptr, *pend_fb = nullptr;
+  auto join_into = [&](LnQuantJob &j, bool write) {
+    j.ja = m->attn;
+    j.jab = pend_ab;
+    j.jf = m->ff;
+    j.jfb = pend_fb;
+    j.jout = write ? R[cur ^ 1] : nullptr;
+  };
   for (int il = m->l0; il < m->l1; ++il) {
     const LayerW &L = m->layers[il - m->l0];
     const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
-    // 1. input LayerNorm (+ post_attention LayerNorm for GPT-NeoX), quantized
-    const LnQuantJob j1{m->inpL, L.ln1_w, L.ln1_b, q1, d1, m->xd1};
-    const LnQuantJob j2{m->inpL, L.ln2_w, L.ln2_b, q2, d2, m->xd2};
+    // 1. (join of the previous layer +) input LayerNorm (+ post_attention LayerNorm for
+    //    GPT-NeoX), quantized
+    LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
+    LnQuantJob j2{R[cur], L.ln2_w, L.ln2_b, q2, d2, m->xd2};
+    if (pending) {
+      join_into(j1, true);
+      join_into(j2, false);
+    }
     RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
     ++nk;
+    if (pending) cur ^= 1;
     // 2. {fc_in (+bias, GELU, requantize), Q, K, V (+bias)}
     GemvBatch B{};
     B.nj = 4;
-    auto job = [&](int i, void *W, int M, int K, const float *xd, const uint8_t *xq, const float *xdd,
+    auto job = [&](GemvBatch &Bt, int i, void *W, int M, int K, const float *xd, const uint8_t *xq, const float *xdd,
                    const float *bias, float *y) {
-      GemvJob &J = B.j[i];
+      GemvJob &J = Bt.j[i];
       J.w = w4_view(W, M, K);
       J.xd = xd;
       J.xqs = xq;
@@ -418,15 +443,15 @@ int enqueue_decode(vsim_model *m, int &nk) {
       J.y = y;
       J.epi = EPI_STORE;
     };
-    job(0, L.wfc, F, E, gptj ? m->xd1 : m->xd2, gptj ? q1 : q2, gptj ? d1 : d2, L.bfc, nullptr);
+    job(B, 0, L.wfc, F, E, gptj ? m->xd1 : m->xd2, gptj ? q1 : q2, gptj ? d1 : d2, L.bfc, nullptr);
     B.j[0].epi = EPI_GELU_Q;
     B.j[0].gelu_tab = tab.gelu_f16;
     B.j[0].oq_qs = q3;
     B.j[0].oq_d = d3;
     B.j[0].oxd = m->xd3;
-    job(1, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
-    job(2, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
-    job(3, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
+    job(B, 1, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
+    job(B, 2, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
+    job(B, 3, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
     hipEvent_t *ev = prof_begin(m);
     RC(launch_gemv_epi(B, m->mode, s));
     prof_end(m, ev, w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
@@ -452,28 +477,26 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.out = nullptr;
     RC(launch_attn_decode(A, m->n_ctx, s));
     ++nk;
-    // 4. out-projection + fc_out + residual
-    DualJob D{};
-    D.a = w4_view(L.wo, E, E);
-    D.b = w4_view(L.wproj, E, F);
-    D.xda = m->xda;
-    D.xdb = m->xd3;
-    D.xqa = qa;
-    D.xqb = q3;
-    D.xdda = da;
-    D.xddb = d3;
-    D.bias_a = gptj ? nullptr : L.bo;
-    D.bias_b = L.bproj;
-    D.inpL = m->inpL;
+    // 4. {fc_out, out-projection} without biases (they join in the next norm); fc_out first
+    //    so its longer chains start first
+    GemvBatch B2{};
+    B2.nj = 2;
+    job(B2, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
+    job(B2, 1, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
     ev = prof_begin(m);
-    RC(launch_gemv_dual(D, m->mode, s));
-    prof_end(m, ev, w4_algo_bytes(D.a) + w4_algo_bytes(D.b));
+    RC(launch_gemv_epi(B2, m->mode, s));
+    prof_end(m, ev, w4_algo_bytes(B2.j[0].w) + w4_algo_bytes(B2.j[1].w));
     ++nk;
+    pending = true;
+    pend_ab = gptj ? nullptr : L.bo;
+    pend_fb = L.bproj;
   }
   if (m->last) {
-    const LnQuantJob jf{m->inpL, m->lnf_w, m->lnf_b, q1, d1, m->xd1};
+    LnQuantJob jf{R[cur], m->lnf_w, m->lnf_b, q1, d1, m->xd1};
+    if (pending) join_into(jf, true);
     RC(launch_ln_quant(jf, nullptr, E, s));
     ++nk;
+    if (pending) cur ^= 1;
     GemvBatch B{};
     B.nj = 1;
     B.j[0].w = w4_view(m->lmh, V, E);
@@ -487,7 +510,12 @@ int enqueue_decode(vsim_model *m, int &nk) {
     RC(launch_gemv_epi(B, m->mode, s));
     prof_end(m, ev, w4_algo_bytes(B.j[0].w));
     ++nk;
+  } else if (pending) {
+    RC(launch_residual_join(R[cur], m->attn, pend_ab, m->ff, pend_fb, R[cur ^ 1], E, s));
+    ++nk;
+    cur ^= 1;
   }
+  m->resid_final = R[cur];
   return VSIM_OK;
 }
 
@@ -771,7 +799,7 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
       if (m->last && logits)
         VSIM_HIP(hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s));
       else if (!m->last && resid_out)
-        VSIM_HIP(hipMemcpyAsync(resid_out, m->inpL, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+        VSIM_HIP(hipMemcpyAsync(resid_out, m->resid_final, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
     }
   } else {
     // general path: prompt batches (N > 1) and the serial-residual GPT-NeoX variant
