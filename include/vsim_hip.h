@@ -96,6 +96,9 @@ int vsim_op_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream);
 /* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);
+/* cumulative counts of exact-LayerNorm rows that needed the sequential fallback:
+ * out[0] = mean not certified, out[1] = variance scale not certified (device-wide) */
+int vsim_norm_fallbacks(unsigned out[2]);
 int vsim_op_gelu(const float *x, float *y, int n, void *stream);
 /* scale -> diag_mask_inf(n_past) -> soft_max over p[nz][nr][nc], in place */
 int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream);

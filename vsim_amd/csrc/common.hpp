@@ -158,25 +158,58 @@ __device__ __forceinline__ int x86_round_i8(float v) {
 }
 
 // ---------------------------------------------------------------- wave reductions
+// Butterfly/broadcast steps in DPP (a few cycles each instead of an LDS permute round trip):
+// quad_perm xor 1 and 2, row_half_mirror (8), row_mirror (16), row_bcast15 and row_bcast31
+// (upper rows only), which leaves the full reduction in lane 63; readlane broadcasts it.
+// Every caller combines values whose result is independent of the order (exact sums,
+// min/max, or a sum whose rounding is bounded by a certificate).
+namespace dpp {
+constexpr int QP_XOR1 = 0xB1, QP_XOR2 = 0x4E, HALF_MIRROR = 0x141, MIRROR = 0x140, BCAST15 = 0x142, BCAST31 = 0x143;
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int mov(int v, int identity) {
+  return __builtin_amdgcn_update_dpp(identity, v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double mov(double v, double identity) {
+  const long long b = __double_as_longlong(v), ib = __double_as_longlong(identity);
+  const int lo = mov<CTRL, ROWS>((int)(b & 0xFFFFFFFF), (int)(ib & 0xFFFFFFFF));
+  const int hi = mov<CTRL, ROWS>((int)(b >> 32), (int)(ib >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float mov(float v, float identity) {
+  return __int_as_float(mov<CTRL, ROWS>(__float_as_int(v), __float_as_int(identity)));
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T reduce(T v, T identity, Op op) {
+  v = op(v, mov<QP_XOR1, 0xF>(v, identity));
+  v = op(v, mov<QP_XOR2, 0xF>(v, identity));
+  v = op(v, mov<HALF_MIRROR, 0xF>(v, identity));
+  v = op(v, mov<MIRROR, 0xF>(v, identity));
+  v = op(v, mov<BCAST15, 0xA>(v, identity));
+  v = op(v, mov<BCAST31, 0xC>(v, identity));
+  return v;  // lane 63 holds the reduction
+}
+__device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
+__device__ __forceinline__ float lane63(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+__device__ __forceinline__ double lane63(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFF), 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+}  // namespace dpp
+
 __device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return dpp::lane63(dpp::reduce(v, 0.0f, [](float a, float b) { return a + b; }));
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return dpp::lane63(dpp::reduce(v, 0.0, [](double a, double b) { return a + b; }));
 }
 __device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return dpp::lane63(dpp::reduce(v, -INFINITY, [](float a, float b) { return fmaxf(a, b); }));
 }
 __device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
+  return dpp::lane63(dpp::reduce(v, 0x7FFFFFFF, [](int a, int b) { return min(a, b); }));
 }
 
 // ---------------------------------------------------------------- errors
@@ -194,7 +227,8 @@ struct DevTables {
   const uint16_t *exp_f16;   // table_exp_f16 (ggml.c:1249)
   const uint16_t *gelu_f16;  // table_gelu_f16 (ggml.c:1247)
 };
-int tables_get(DevTables *t);  // lazily uploads host-built tables for the current device
+int tables_get(DevTables *t);
+int norm_stats(unsigned *out2);  // LayerNorm fallback counters (ops_elt.hip)  // lazily uploads host-built tables for the current device
 
 int launch_q4_repack(const void *aos, void *soa, int rows, int k, hipStream_t s);
 int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s);

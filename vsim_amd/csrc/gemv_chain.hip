@@ -101,32 +101,6 @@ __device__ __forceinline__ void chain_rows(const GemvBatch &B, ChainRows &S) {
   }
 }
 
-// Quantize one 32-value block per half-wave (lanes 0-31 -> block A, 32-63 -> block B) with
-// quantize_row_q4_0 semantics (see quantize_block_lanes in kern.hpp).
-__device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
-                                              float *xd_out) {
-  float a = fabsf(v);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    const float t = __shfl_xor(a, o, 64);
-    a = a > t ? a : t;
-  }
-  const float d = a / 7.0f;
-  const float id = d != 0.0f ? 1.0f / d : 0.0f;
-  const int q = x86_round_i8(v * id) + 8;
-  const int l = lane & 31;
-  const int qn = __shfl_xor(q, 1, 64);
-  const uint32_t byte = (l & 1) ? 0u : (uint32_t)((q & 0xF) | ((qn & 0xF) << 4));
-  uint32_t word = byte << (8 * ((l >> 1) & 3));
-  word |= __shfl_xor(word, 2, 64);
-  word |= __shfl_xor(word, 4, 64);
-  if (ok) {
-    if ((l & 7) == 0) ((uint32_t *)qs_out)[l >> 3] = word;
-    if (l == 0) *d_out = d;
-    xd_out[l] = d * (float)(q - 8);
-  }
-}
-
 // timing experiment output (DBG & 8): [0..3] producer wave 0 of block 0, [4] iterations,
 // [8..9] consumer of block 0 (cycles summed over iterations)
 __device__ unsigned long long g_chain_prof[64];

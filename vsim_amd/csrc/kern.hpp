@@ -131,37 +131,12 @@ __device__ __forceinline__ int ulp_exp(float x) {
   return e == 0 ? -149 : e - 150;
 }
 
-template <typename T>
-__device__ T block_sum(T v, T *sh) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if (lane == 0) sh[wid] = v;
-  __syncthreads();
-  T r = 0;
-  for (int w = 0; w < NORM_THREADS / 64; ++w) r += sh[w];
-  return r;
-}
-
-__device__ int block_min(int v, int *sh) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  v = wave_min_i(v);
-  __syncthreads();
-  if (lane == 0) sh[wid] = v;
-  __syncthreads();
-  int r = sh[0];
-  for (int w = 1; w < NORM_THREADS / 64; ++w) r = min(r, sh[w]);
-  return r;
-}
-
-
 }  // namespace vsim
 
 namespace vsim {
 
 // ------------------------------------------------------------------ exact LayerNorm core
-// ggml_compute_forward_norm_f32 (ggml.c:4246-4304) for one row by one 256-thread block,
+// ggml_compute_forward_norm_f32 (ggml.c:4246-4304) for one row by one NT-thread block,
 // result left in `row` (LDS, n floats, in place).  The reference sums sequentially in
 // double; we sum in parallel and prove the sum equal to the sequential one, falling back
 // to the sequential loop otherwise:
@@ -171,44 +146,79 @@ namespace vsim {
 //    (2n+64)*2^-53*sum(w); if both ends of that interval give the same float scale
 //    (the map S -> (float)(1/sqrt(S/n+eps)) is monotone) the scale is the reference's.
 // Optional affine y = w*y + b (ggml_add(ggml_mul(repeat(w), cur), repeat(b))).
-// stats (optional): [0] mean fallbacks, [1] variance fallbacks.
 // Optional residual join first (the previous layer's, vsim.cpp:694-695): the normalized row is
 // v = x + ((ja + jab) + (jf + jfb)) (jab may be null), written to jout when jout != null.
-struct LnJoin {
-  const float *ja, *jab, *jf, *jfb;
-  float *jout;
-};
-
-__device__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
-                             const float *__restrict__ gb, unsigned *stats, const LnJoin *J = nullptr) {
-  __shared__ double shd[NORM_THREADS / 64];
-  __shared__ int shi[NORM_THREADS / 64];
+// stats (optional): [0] mean fallbacks, [1] variance fallbacks.
+// n % 4 == 0; float4 accesses, NT threads x 4 elements per pass, so for n <= 4*NT every load
+// of a pass issues at once (a loop of scalar loads behind branches serialized on their
+// latency and dominated the kernel).
+template <int NT>
+__device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
+                               const float *__restrict__ gb, unsigned *stats, const float *__restrict__ ja = nullptr,
+                               const float *__restrict__ jab = nullptr, const float *__restrict__ jf = nullptr,
+                               const float *__restrict__ jfb = nullptr, float *__restrict__ jout = nullptr) {
+  constexpr int NW = NT / 64;
+  __shared__ double shs[NW], shsa[NW];
+  __shared__ int shu[NW];
   __shared__ double bcast_d;
   __shared__ float bcast_f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n4 = n / 4;
   const double eps = 1e-5f;
   double s = 0.0, sa = 0.0;
   int um = 1 << 30;
-  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    float v = x[i];
-    if (J) {
-      const float attn = J->jab ? J->ja[i] + J->jab[i] : J->ja[i];
-      const float ff = J->jf[i] + J->jfb[i];
-      v = v + (attn + ff);
-      if (J->jout) J->jout[i] = v;
+  for (int i = threadIdx.x; i < n4; i += NT) {
+    float4 v = ((const float4 *)x)[i];
+    if (ja) {
+      float4 a = ((const float4 *)ja)[i];
+      const float4 f = ((const float4 *)jf)[i], fb = ((const float4 *)jfb)[i];
+      if (jab) {
+        const float4 ab = ((const float4 *)jab)[i];
+        a = make_float4(a.x + ab.x, a.y + ab.y, a.z + ab.z, a.w + ab.w);
+      }
+      v = make_float4(v.x + (a.x + (f.x + fb.x)), v.y + (a.y + (f.y + fb.y)), v.z + (a.z + (f.z + fb.z)),
+                      v.w + (a.w + (f.w + fb.w)));
+      if (jout) ((float4 *)jout)[i] = v;
     }
-    row[i] = v;
-    s += (double)v;
-    sa += (double)fabsf(v);
-    um = min(um, ulp_exp(v));
+    ((float4 *)row)[i] = v;
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s += (double)e[j];
+      sa += (double)fabsf(e[j]);
+      um = min(um, ulp_exp(e[j]));
+    }
   }
-  s = block_sum(s, shd);
-  sa = block_sum(sa, shd);
-  um = block_min(um, shi);
+  s = wave_sum_d(s);
+  sa = wave_sum_d(sa);
+  um = wave_min_i(um);
+  if (lane == 0) {
+    shs[wid] = s;
+    shsa[wid] = sa;
+    shu[wid] = um;
+  }
+  __syncthreads();
+  s = 0.0;
+  sa = 0.0;
+  um = 1 << 30;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    s += shs[w];
+    sa += shsa[w];
+    um = min(um, shu[w]);
+  }
   const bool exact = (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
   if (!exact) {
+    // sequential fallback, 4 independent partial loads per step to keep the LDS reads ahead
     if (threadIdx.x == 0) {
       double m = 0.0;
-      for (int i = 0; i < n; ++i) m += row[i];
+      for (int i = 0; i < n4; ++i) {
+        const float4 v = ((const float4 *)row)[i];
+        m += v.x;
+        m += v.y;
+        m += v.z;
+        m += v.w;
+      }
       bcast_d = m;
       if (stats) atomicAdd(&stats[0], 1u);
     }
@@ -217,11 +227,22 @@ __device__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, con
   }
   const double mean = s / n;
   double s2 = 0.0;
-  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    const double v = (double)row[i] - mean;
-    s2 += v * v;
+  for (int i = threadIdx.x; i < n4; i += NT) {
+    const float4 v4 = ((const float4 *)row)[i];
+    const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double v = (double)e[j] - mean;
+      s2 += v * v;
+    }
   }
-  s2 = block_sum(s2, shd);
+  s2 = wave_sum_d(s2);
+  __syncthreads();  // everyone has read shs above
+  if (lane == 0) shs[wid] = s2;
+  __syncthreads();
+  s2 = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) s2 += shs[w];
   const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
   const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
   const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
@@ -239,14 +260,56 @@ __device__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, con
     __syncthreads();
     scale = bcast_f;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += NORM_THREADS) {
-    float v = (float)((double)row[i] - mean);
-    v = v * scale;
-    if (gw) v = (gw[i] * v) + gb[i];
-    row[i] = v;
+  for (int i = threadIdx.x; i < n4; i += NT) {
+    const float4 v4 = ((const float4 *)row)[i];
+    float e[4] = {v4.x, v4.y, v4.z, v4.w};
+    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = w4;
+    if (gw) {
+      w4 = ((const float4 *)gw)[i];
+      b4 = ((const float4 *)gb)[i];
+    }
+    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = (float)((double)e[j] - mean);
+      v = v * scale;
+      if (gw) v = (wv[j] * v) + bv[j];
+      e[j] = v;
+    }
+    ((float4 *)row)[i] = make_float4(e[0], e[1], e[2], e[3]);
   }
   __syncthreads();
+}
+
+__device__ __forceinline__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
+                                             const float *__restrict__ gb, unsigned *stats) {
+  ln_exact_lds_t<NORM_THREADS>(x, row, n, gw, gb, stats);
+}
+
+// Quantize one 32-value block per half-wave (lanes 0-31 -> block A, 32-63 -> block B) with
+// quantize_row_q4_0 semantics (see quantize_block_lanes below).
+__device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
+                                              float *xd_out) {
+  float a = fabsf(v);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    const float t = __shfl_xor(a, o, 64);
+    a = a > t ? a : t;
+  }
+  const float d = a / 7.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  const int q = x86_round_i8(v * id) + 8;
+  const int l = lane & 31;
+  const int qn = __shfl_xor(q, 1, 64);
+  const uint32_t byte = (l & 1) ? 0u : (uint32_t)((q & 0xF) | ((qn & 0xF) << 4));
+  uint32_t word = byte << (8 * ((l >> 1) & 3));
+  word |= __shfl_xor(word, 2, 64);
+  word |= __shfl_xor(word, 4, 64);
+  if (ok) {
+    if ((l & 7) == 0) ((uint32_t *)qs_out)[l >> 3] = word;
+    if (l == 0) *d_out = d;
+    xd_out[l] = d * (float)(q - 8);
+  }
 }
 
 // Quantize one 32-element block held by lanes 0..31 of a wave (value v in lane l = element

@@ -24,22 +24,24 @@ namespace vsim {
 extern unsigned *g_norm_stats;
 
 // ------------------------------------------------------------------ 1. LN + quantize
-__global__ void __launch_bounds__(NORM_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
+// One 1024-thread workgroup per LayerNorm (two for GPT-NeoX's parallel-residual pair); the
+// normalized row is quantized by whole waves, two 32-blocks per wave step.
+constexpr int LNQ_THREADS = 1024;
+__global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float row[];
-  const LnQuantJob J = blockIdx.x == 0 ? j0 : j1;
-  const LnJoin jn{J.ja, J.jab, J.jf, J.jfb, J.jout};
-  ln_exact_lds(J.x, row, n, J.w, J.b, stats, J.ja ? &jn : nullptr);
-  const int nb = n / QK;
-  for (int b = threadIdx.x; b < nb; b += NORM_THREADS) {
-    float v[QK];
-#pragma unroll
-    for (int l = 0; l < QK; ++l) v[l] = row[b * QK + l];
-    quantize_block(v, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
+  const LnQuantJob &J = blockIdx.x == 0 ? j0 : j1;
+  ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, stats, J.ja, J.jab, J.jf, J.jfb, J.jout);
+  const int nb = n / QK, lane = threadIdx.x & 63;
+  for (int b2 = threadIdx.x >> 6; 2 * b2 < nb; b2 += LNQ_THREADS / 64) {
+    const int b = 2 * b2 + (lane >> 5);
+    const bool ok = b < nb;
+    const float v = ok ? row[b * QK + (lane & 31)] : 0.0f;
+    quantize_half(v, lane, ok, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
   }
 }
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_ln_quant, dim3(j1 ? 2 : 1), dim3(NORM_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
+  hipLaunchKernelGGL(k_ln_quant, dim3(j1 ? 2 : 1), dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
                      g_norm_stats);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
@@ -341,7 +343,14 @@ int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ 3. attention (N = 1)
-constexpr int ATT_THREADS = 256;
+// One 1024-thread workgroup per head.  KQ: one wave per key, products over the head
+// dimension summed as a tree in double; the reference's sequential double sum lies within
+// 2*d*2^-53*sum|p| of it, so when both ends of that interval round to the same float the
+// score is the reference's, otherwise lane 0 redoes the key sequentially (ggml.c:4760-4800
+// for the f32 dot with a double accumulator).  KQV keeps the reference's sequential float
+// chain over the keys, one chain per output element.
+constexpr int ATT_THREADS = 1024;
+constexpr int ATT_WAVES = ATT_THREADS / 64;
 
 __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -351,8 +360,8 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   float *qh = sm;           // [d]
   float *kh = sm + d;       // [d]
   float *pr = sm + 2 * d;   // [nk] scores / probabilities
-  __shared__ float shf[ATT_THREADS / 64];
-  __shared__ double shd[ATT_THREADS / 64];
+  __shared__ float shf[ATT_WAVES];
+  __shared__ double shd[ATT_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < d; i += ATT_THREADS) {
     qh[i] = A.q[h * d + i];
@@ -382,22 +391,26 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   for (int i = tid; i < d; i += ATT_THREADS) A.kc[(size_t)n_past * E + h * d + i] = kh[i];
   // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale
   float mx = -INFINITY;
-  for (int k = tid; k < nk; k += ATT_THREADS) {
+  for (int k = wid; k < nk; k += ATT_WAVES) {
     const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
-    double acc = 0.0;
-    if (k == n_past) {
-      for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
-    } else {
-      for (int i = 0; i < d; i += 4) {
-        const float4 a = *(const float4 *)(kr + i);
-        acc += (double)(a.x * qh[i]);
-        acc += (double)(a.y * qh[i + 1]);
-        acc += (double)(a.z * qh[i + 2]);
-        acc += (double)(a.w * qh[i + 3]);
-      }
+    double t = 0.0, ta = 0.0;
+    for (int i = lane; i < d; i += 64) {
+      const double p = (double)(kr[i] * qh[i]);
+      t += p;
+      ta += fabs(p);
     }
-    const float sc = (float)acc * A.scale;
-    pr[k] = sc;
+    t = wave_sum_d(t);
+    ta = wave_sum_d(ta);
+    const double bnd = 2.0 * d * 0x1.0p-53 * ta;
+    float sc = (float)(t - bnd);
+    if (sc != (float)(t + bnd)) {  // wave-uniform: redo this key in the reference order
+      double acc = 0.0;
+      if (lane == 0)
+        for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
+      sc = (float)__shfl(acc, 0, 64);
+    }
+    sc = sc * A.scale;
+    if (lane == 0) pr[k] = sc;
     mx = mx > sc ? mx : sc;
   }
   // max, exp via table, exact double sum (fp16 values: any order), 1/sum
@@ -405,7 +418,7 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   if (lane == 0) shf[wid] = mx;
   __syncthreads();
   mx = shf[0];
-  for (int w = 1; w < ATT_THREADS / 64; ++w) mx = mx > shf[w] ? mx : shf[w];
+  for (int w = 1; w < ATT_WAVES; ++w) mx = mx > shf[w] ? mx : shf[w];
   double sum = 0.0;
   for (int k = tid; k < nk; k += ATT_THREADS) {
     const float val = h2f(A.etab[f2h(pr[k] - mx)]);
@@ -415,28 +428,34 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   sum = wave_sum_d(sum);
   if (lane == 0) shd[wid] = sum;
   __syncthreads();
-  sum = (shd[0] + shd[1]) + (shd[2] + shd[3]);
+  sum = 0.0;
+  for (int w = 0; w < ATT_WAVES; ++w) sum += shd[w];
   const float inv = (float)(1.0 / sum);
   for (int k = tid; k < nk; k += ATT_THREADS) pr[k] = pr[k] * inv;
   __syncthreads();
-  // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f
+  // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f; V rows loaded
+  // 16 keys ahead of the chain
   for (int dd0 = 0; dd0 < d; dd0 += ATT_THREADS) {
     const int dd = dd0 + tid;
     float y = 0.0f;
     if (dd < d) {
       const float *vcol = A.vc + h * d + dd;
-      for (int k = 0; k < nk; ++k) y = y + vcol[(size_t)k * E] * pr[k];
+      int k = 0;
+      for (; k + 16 <= nk; k += 16) {
+        float vv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) vv[j] = vcol[(size_t)(k + j) * E];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) y = y + vv[j] * pr[k + j];
+      }
+      for (; k < nk; ++k) y = y + vcol[(size_t)k * E] * pr[k];
       if (A.out) A.out[h * d + dd] = y;
     }
-    // quantize each 32-block of this head's output (wave-sized pieces of the d outputs)
-    const int blk = (h * d + dd0 + wid * 64) / QK;
+    // quantize the head's outputs, two 32-blocks per wave
     if (dd0 + wid * 64 < d) {
-      quantize_block_lanes(y, lane, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
-      // lanes 32..63 of the wave hold the next block
-      const float y2 = __shfl_down(y, 32, 64);
-      if (dd0 + wid * 64 + 32 < d)
-        quantize_block_lanes(lane < 32 ? y2 : 0.0f, lane, A.oq_qs + (size_t)(blk + 1) * 16, A.oq_d + blk + 1,
-                             A.oxd + (size_t)(blk + 1) * QK);
+      const int blk = (h * d + dd0 + wid * 64) / QK + (lane >> 5);
+      const bool ok = dd0 + wid * 64 + (lane & ~31) < d;
+      quantize_half(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
     }
   }
 }

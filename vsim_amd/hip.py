@@ -25,7 +25,7 @@ EXPORTS = [
     "vsim_last_error", "vsim_device_count", "vsim_q4_bytes",
     "init_xmax", "imax_ggml_compute_forward_mul_mat_q4_0_f32",
     "vsim_ggml_gptneox_rope_f32", "vsim_ggml_rope_f32", "vsim_ggml_soft_max_f32", "vsim_ggml_mul_mat_f32",
-    "vsim_dropin_stats", "vsim_dropin_reset",
+    "vsim_dropin_stats", "vsim_dropin_reset", "vsim_norm_fallbacks",
     "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_act_repack", "vsim_op_act_unpack",
     "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_get_rows",
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
@@ -190,6 +190,13 @@ class Model:
             self.close()
         except Exception:
             pass
+
+
+def norm_fallbacks():
+    """Exact-LayerNorm rows that took the sequential fallback so far: (mean, variance)."""
+    out = (ctypes.c_uint * 2)()
+    check(lib().vsim_norm_fallbacks(out), "norm_fallbacks")
+    return int(out[0]), int(out[1])
 
 
 def dropin_stats():
