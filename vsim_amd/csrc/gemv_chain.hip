@@ -292,6 +292,172 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
   }
 }
 
+// ================================================================== 32-row variant
+// Same chain and producer/consumer protocol for one W4T32 tile (32 rows) per workgroup, so a
+// job with few rows spreads over more CUs (fc_out: 128 workgroups instead of 64) and each
+// CU's producers carry half the work.  4 producer waves, each 2 blocks of the 8-block chunk
+// (lanes 0-31: rows of block 2p, lanes 32-63: rows of block 2p+1); the activation factors
+// then differ between the two half-waves, so they come through the LDS ring as well (one
+// LDS-DMA per chunk by the first producer, read with per-half broadcast loads) instead of
+// scalar loads.
+constexpr int C2_CB = 8, C2_CP = C2_CB * 16, C2_LD = C2_CP + 4, C2_NPW = C2_CB / 2;
+constexpr int C2_THREADS = 64 * (1 + C2_NPW);
+constexpr int C2_RING = 3, C2_WIN = 8, C2_DEPTH = 4, C2_RAW = C2_DEPTH;  // raw slot reuse: see below
+constexpr int C2_WAIT_VM3 = 0x0F70 | (3 * (C2_DEPTH - 2));  // wave 1: nibbles, scales, factors
+constexpr int C2_WAIT_VM2 = 0x0F70 | (2 * (C2_DEPTH - 2));  // other producers: nibbles, scales
+static_assert(3 * (C2_DEPTH - 2) < 16, "vmcnt immediate");
+
+template <int DBG>
+__global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
+  __shared__ __attribute__((aligned(16))) float P[C2_RING][32 * C2_LD];
+  __shared__ __attribute__((aligned(16))) uint4 RQ[C2_RAW][C2_NPW][64];
+  __shared__ __attribute__((aligned(16))) float RD[C2_RAW][C2_NPW][64];
+  __shared__ __attribute__((aligned(16))) float RX[C2_RAW][C2_CB * QK];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  int t = blockIdx.x, ji = 0;
+  while (ji < B.nj) {
+    if (t < B.j[ji].w.tiles) break;
+    t -= B.j[ji].w.tiles;
+    ++ji;
+  }
+  if (ji >= B.nj) return;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const int nb = B.j[ji].w.k / QK, nch = (nb + C2_CB - 1) / C2_CB;
+  const int nit = (nch + 2 + 1) & ~1;
+  const uint8_t *tqs = B.j[ji].w.qs + (size_t)t * nb * T32 * 16;
+  const float *td = B.j[ji].w.d + (size_t)t * nb * T32;
+  const float *x = B.j[ji].xd;
+
+  if (wave > 0) {
+    // ------------------------------------------------------------- producer
+    // Step k (as in k_gemv_chain): read chunk k+1's raw block and factors (landed before the
+    // previous barrier) into registers, LDS-DMA of chunk k+DEPTH, pair terms of chunk k from
+    // the registers filled in step k-1, wait for this wave's DMA of chunk k+2, barrier.
+    // Raw slot reuse: chunk c lives in slot c % RAW; the DMA of chunk k+DEPTH (step k) reuses
+    // the slot of chunk k, whose registers were read in step k-1 (retired at that barrier).
+    const int p = wave - 1, r = lane & 31, hb = lane >> 5;
+    const int o = 2 * p + hb;  // this lane's block within the chunk
+    const uint8_t *qs = tqs + (size_t)r * 16;
+    const float *dd = td + r;
+    auto dma = [&](int c) {
+      const int slot = c % C2_RAW;
+      const int b = min(c * C2_CB + o, nb - 1);
+      glds16(qs + (size_t)b * (T32 * 16), lds_addr(&RQ[slot][p][0]));
+      glds4(dd + (size_t)b * T32, lds_addr(&RD[slot][p][0]));
+      if (p == 0) {  // the chunk's 8 x 32 activation factors, 16 bytes per lane (clamped block)
+        const int bx = min(c * C2_CB + (lane >> 3), nb - 1);
+        glds16(x + (size_t)bx * QK + 4 * (lane & 7), lds_addr(&RX[slot][0]));
+      }
+    };
+    auto ldraw = [&](int c, uint4 &q, float &dq, f32x2 *xv) {
+      const int slot = c % C2_RAW;
+      q = RQ[slot][p][lane];
+      dq = RD[slot][p][lane];
+      const float4 *xp = (const float4 *)&RX[slot][o * QK];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 v = xp[i];
+        xv[2 * i].x = v.x;
+        xv[2 * i].y = v.y;
+        xv[2 * i + 1].x = v.z;
+        xv[2 * i + 1].y = v.w;
+      }
+    };
+    int ps = 0;
+    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const uint4 &qc, float dqc, uint4 &qn, float &dqn) {
+      ldraw(k + 1, qn, dqn, xn);
+      if (!(DBG & 4)) dma(k + C2_DEPTH);
+      if (!(DBG & 2)) {
+        const float dv = k * C2_CB + o < nb ? dqc : 0.0f;
+        const f32x2 d2 = {dv, dv}, m2 = {-8.0f * dv, -8.0f * dv};
+        float *dst = &P[ps][r * C2_LD + o * 16];
+        const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) {
+          float p4[4];
+          pair_terms4_fma(qw[wv], d2, m2, xc + 4 * wv, p4);
+          *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+        }
+      }
+      ps = ps == C2_RING - 1 ? 0 : ps + 1;
+      if (p == 0)  // this wave's DMA of chunk k+2 landed
+        __builtin_amdgcn_s_waitcnt(C2_WAIT_VM3);
+      else
+        __builtin_amdgcn_s_waitcnt(C2_WAIT_VM2);
+      __syncthreads();
+    };
+#pragma unroll
+    for (int c = 0; c < C2_DEPTH; ++c) dma(c);
+    f32x2 xa[16], xb[16];
+    uint4 qa, qb;
+    float da, db;
+    if (p == 0)  // chunks 0 and 1 landed
+      __builtin_amdgcn_s_waitcnt(C2_WAIT_VM3);
+    else
+      __builtin_amdgcn_s_waitcnt(C2_WAIT_VM2);
+    __syncthreads();
+    ldraw(0, qa, da, xa);
+    __syncthreads();
+    for (int k = 0; k < nit; k += 2) {
+      step(k, xa, xb, qa, da, qb, db);
+      step(k + 1, xb, xa, qb, db, qa, da);
+    }
+    return;
+  }
+
+  // --------------------------------------------------------------- consumer (lanes 0-31)
+  float acc = 0.0f;
+  float4 win[C2_WIN];
+  const int lr = lane & 31;
+  auto src = [&](int c) { return &P[c % C2_RING][lr * C2_LD]; };
+  __builtin_amdgcn_s_setprio(3);
+  __syncthreads();
+  __syncthreads();
+  for (int k = 0; k < nit; ++k) {
+    const int c = k - 2;
+    if (c == -1 && nch > 0) {
+      const float *p0 = src(0);
+#pragma unroll
+      for (int j = 0; j < C2_WIN; ++j) win[j] = *(const float4 *)(p0 + 4 * j);
+    } else if (c >= 0 && c < nch) {
+      const float *pc = src(c), *pn = src(c + 1);
+#pragma unroll
+      for (int j = 0; j < C2_CP / 4; ++j) {
+        const float4 v = win[j % C2_WIN];
+        if (!(DBG & 1)) {
+          acc = acc + v.x;
+          acc = acc + v.y;
+          acc = acc + v.z;
+          acc = acc + v.w;
+        }
+        const int jn = j + C2_WIN;
+        win[j % C2_WIN] = jn < C2_CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - C2_CP / 4));
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ----------------------------------------------------------------- epilogue
+  const int row = t * T32 + lr;
+  const int rows = B.j[ji].w.rows;
+  const float *bias = B.j[ji].bias;
+  float *y = B.j[ji].y;
+  if (B.j[ji].epi == EPI_GELU_Q) {
+    const bool ok = lane < 32 && row < rows;
+    float g = 0.0f;
+    if (ok) {
+      g = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      if (y) y[row] = g;
+    }
+    quantize_half(g, lane, ok, B.j[ji].oq_qs + (size_t)t * 16, B.j[ji].oq_d + t, B.j[ji].oxd + (size_t)t * QK);
+  } else if (lane < 32 && row < rows) {
+    y[row] = bias ? acc + bias[row] : acc;
+  }
+}
+
 template <int DBG>
 static void chain_launch_t(int grid, const GemvBatch &B, hipStream_t s) {
   hipLaunchKernelGGL(k_gemv_chain<DBG>, dim3(grid), dim3(CH_THREADS), 0, s, B);
@@ -308,10 +474,31 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     groups += (B.j[i].w.tiles + 1) / 2;
   }
   if (groups == 0) return VSIM_OK;
+  static const int variant = [] {
+    const char *e = getenv("VSIM_CHAIN_ROWS");
+    return e ? atoi(e) : 0;
+  }();
+  int tiles = 0;
+  for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
+  // 32-row workgroups when the 64-row grid would leave most CUs without a chain
+  const bool narrow = variant == 32 || (variant != 64 && groups < 192);
   static const int dbg = [] {
     const char *e = getenv("VSIM_CHAIN_DBG");
     return e ? atoi(e) : 0;
   }();
+  if (narrow) {
+    switch (dbg) {
+      case 1: hipLaunchKernelGGL(k_gemv_chain32<1>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+      case 2: hipLaunchKernelGGL(k_gemv_chain32<2>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+      case 4: hipLaunchKernelGGL(k_gemv_chain32<4>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+      case 5: hipLaunchKernelGGL(k_gemv_chain32<5>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+      case 6: hipLaunchKernelGGL(k_gemv_chain32<6>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+      case 7: hipLaunchKernelGGL(k_gemv_chain32<7>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+      default: hipLaunchKernelGGL(k_gemv_chain32<0>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+    }
+    VSIM_HIP(hipGetLastError());
+    return VSIM_OK;
+  }
   switch (dbg) {
     case 1: chain_launch_t<1>(groups, B, s); break;
     case 2: chain_launch_t<2>(groups, B, s); break;
