@@ -30,11 +30,9 @@
 
 namespace vsim {
 
-constexpr int CH_CB = 8;                 // Q4_0 blocks per chunk
-constexpr int CH_CP = CH_CB * 16;        // pairs per row per chunk
-constexpr int CH_LD = CH_CP + 4;         // LDS row stride (floats): conflict-free b128 access
-constexpr int CH_NPW = CH_CB;            // producer waves: one per block of the chunk
-constexpr int CH_THREADS = 64 * (1 + CH_NPW);
+// template CB: Q4_0 blocks per chunk = producer waves (one per block); a chunk is CB*16
+// pairs per row, its LDS row stride CB*16+4 floats (conflict-free 16-byte access).  CB = 8
+// (152 KB LDS, one workgroup per CU) for few rows, CB = 4 (77 KB, two per CU) for many.
 constexpr int CH_RING = 3;               // pair-term ring slots
 constexpr int CH_WIN = 8;                // consumer read-ahead (16-byte reads)
 constexpr int CH_DEPTH = 4;              // LDS-DMA prefetch depth (chunks)
@@ -107,17 +105,18 @@ __device__ unsigned long long g_chain_prof[64];
 
 // DBG (timing experiments only; results are wrong unless 0 or 8): bit0 = the consumer skips
 // the adds, bit1 = producers skip the pair terms, bit2 = producers skip the LDS-DMA
-template <int DBG>
-__global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
-  __shared__ __attribute__((aligned(16))) float P[CH_RING][64 * CH_LD];
-  __shared__ __attribute__((aligned(16))) uint4 RQ[CH_RAW][CH_CB][64];
-  __shared__ __attribute__((aligned(16))) float RD[CH_RAW][CH_CB][64];
+template <int DBG, int CB>
+__global__ void __launch_bounds__(64 * (1 + CB), 2) k_gemv_chain(GemvBatch B) {
+  constexpr int CP = CB * 16, LD = CP + 4;
+  __shared__ __attribute__((aligned(16))) float P[CH_RING][64 * LD];
+  __shared__ __attribute__((aligned(16))) uint4 RQ[CH_RAW][CB][64];
+  __shared__ __attribute__((aligned(16))) float RD[CH_RAW][CB][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   ChainRows S;
   chain_rows(B, S);
   if (S.job < 0) return;  // whole workgroup: no barrier is reached
-  const int nb = S.nb, nch = (nb + CH_CB - 1) / CH_CB;
+  const int nb = S.nb, nch = (nb + CB - 1) / CB;
   // iterations (one barrier each, after a prologue barrier): chunk k is produced in
   // iteration k and added in k+2; even count for the producers' two x register sets
   const int nit = (nch + 2 + 1) & ~1;
@@ -136,12 +135,12 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
     const float *dd = (tile_ok && h ? S.d1 : S.d0) + r;
     int dslot = 0;  // raw slot of chunk k+DEPTH (advanced per step)
     auto dma = [&](int c, int slot) {  // chunk c, block clamped so every load stays in bounds
-      const int b = min(c * CH_CB + o, nb - 1);
+      const int b = min(c * CB + o, nb - 1);
       glds16(qs + (size_t)b * (T32 * 16), lds_addr(&RQ[slot][o][0]));
       glds4(dd + (size_t)b * T32, lds_addr(&RD[slot][o][0]));
     };
     auto ldx = [&](int c, f32x2 *xv) {  // this item's 32 activation factors (16 pairs)
-      const int b = min(c * CH_CB + o, nb - 1);
+      const int b = min(c * CB + o, nb - 1);
       const sfloat *xp = (const sfloat *)(S.x + (size_t)b * QK);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -164,9 +163,11 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
       }
     };
     int ps = 0;  // P ring slot of chunk k
-    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const uint4 &qc, float dqc, uint4 &qn, float &dqn) {
+    // one set of 32 SGPRs for the factors: chunk k+1's are loaded after chunk k's terms are
+    // done (their latency falls into the barrier wait; a second set costs the compiler
+    // enough SGPRs to force mid-step waits)
+    auto step = [&](int k, f32x2 *x, const uint4 &qc, float dqc, uint4 &qn, float &dqn) {
       stamp(-1);
-      ldx(k + 1, xn);
       rslot = rslot == CH_RAW - 1 ? 0 : rslot + 1;
       ldraw(rslot, qn, dqn);
       if (!(DBG & 4)) dma(k + CH_DEPTH, dslot);
@@ -174,18 +175,20 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
       __builtin_amdgcn_sched_barrier(0);
       stamp(0);
       if (!(DBG & 2)) {
-        const float dv = tile_ok && k * CH_CB + o < nb ? dqc : 0.0f;
+        const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
         const f32x2 d2 = {dv, dv}, m2 = {-8.0f * dv, -8.0f * dv};
-        float *dst = &P[ps][lane * CH_LD + o * 16];
+        float *dst = &P[ps][lane * LD + o * 16];
         const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
 #pragma unroll
         for (int wv = 0; wv < 4; ++wv) {
           float p4[4];
-          pair_terms4_fma(qw[wv], d2, m2, xc + 4 * wv, p4);
+          pair_terms4_fma(qw[wv], d2, m2, x + 4 * wv, p4);
           *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
         }
       }
       ps = ps == CH_RING - 1 ? 0 : ps + 1;
+      __builtin_amdgcn_sched_barrier(0);
+      ldx(k + 1, x);
       stamp(1);
       __builtin_amdgcn_s_waitcnt(WAIT_VM_DEPTH);  // this wave's DMA of chunk k+2 landed
       stamp(2);
@@ -195,17 +198,17 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
 #pragma unroll
     for (int c = 0; c < CH_DEPTH; ++c) dma(c, c);
     dslot = CH_DEPTH % CH_RAW;
-    f32x2 xa[16], xb[16];
+    f32x2 xs[16];
     uint4 qa, qb;
     float da, db;
-    ldx(0, xa);
+    ldx(0, xs);
     __builtin_amdgcn_s_waitcnt(WAIT_VM_DEPTH);  // chunks 0 and 1 landed
     __syncthreads();
     ldraw(0, qa, da);
     __syncthreads();  // (second prologue barrier: the reads above are retired here)
     for (int k = 0; k < nit; k += 2) {
-      step(k, xa, xb, qa, da, qb, db);
-      step(k + 1, xb, xa, qb, db, qa, da);
+      step(k, xs, qa, da, qb, db);
+      step(k + 1, xs, qb, db, qa, da);
     }
     if (prof && lane == 0) {
       for (int i = 0; i < 4; ++i) g_chain_prof[16 + 4 * p + i] = pt[i];
@@ -223,7 +226,7 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
   // window of chunk k-1 (published one barrier earlier; the 3-slot ring keeps both alive).
   float acc = 0.0f;
   float4 win[CH_WIN];
-  auto src = [&](int c) { return &P[c % CH_RING][lane * CH_LD]; };
+  auto src = [&](int c) { return &P[c % CH_RING][lane * LD]; };
   __builtin_amdgcn_s_setprio(3);  // the chain issues first whenever it is ready
   __syncthreads();  // prologue (producers: chunks 0 and 1 landed)
   __syncthreads();  // prologue (producers: raw chunk 0 in registers)
@@ -248,7 +251,7 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
       // chunk's end come from chunk c+1's slot (stale when c+1 == nch, never added)
       const float *pc = src(c), *pn = src(c + 1);
 #pragma unroll
-      for (int j = 0; j < CH_CP / 4; ++j) {
+      for (int j = 0; j < CP / 4; ++j) {
         const float4 v = win[j % CH_WIN];
         if (!(DBG & 1)) {
           acc = acc + v.x;
@@ -257,7 +260,7 @@ __global__ void __launch_bounds__(CH_THREADS, 2) k_gemv_chain(GemvBatch B) {
           acc = acc + v.w;
         }
         const int jn = j + CH_WIN;
-        win[j % CH_WIN] = jn < CH_CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - CH_CP / 4));
+        win[j % CH_WIN] = jn < CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - CP / 4));
         __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read x1
       }
@@ -460,7 +463,9 @@ __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
 
 template <int DBG>
 static void chain_launch_t(int grid, const GemvBatch &B, hipStream_t s) {
-  hipLaunchKernelGGL(k_gemv_chain<DBG>, dim3(grid), dim3(CH_THREADS), 0, s, B);
+  // (CB = 4 at two workgroups per CU measured slower than CB = 8 at one: the producers'
+  // VALU issue per CU, not the grid's rounds, bounds the large batches)
+  hipLaunchKernelGGL((k_gemv_chain<DBG, 8>), dim3(grid), dim3(64 * 9), 0, s, B);
 }
 
 int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {

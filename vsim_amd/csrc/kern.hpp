@@ -167,6 +167,12 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   const double eps = 1e-5f;
   double s = 0.0, sa = 0.0;
   int um = 1 << 30;
+  // affine factors of this thread's first float4, loaded up front (used in the last pass)
+  float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), b0 = w0;
+  if (gw && (int)threadIdx.x < n4) {
+    w0 = ((const float4 *)gw)[threadIdx.x];
+    b0 = ((const float4 *)gb)[threadIdx.x];
+  }
   for (int i = threadIdx.x; i < n4; i += NT) {
     float4 v = ((const float4 *)x)[i];
     if (ja) {
@@ -263,8 +269,8 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   for (int i = threadIdx.x; i < n4; i += NT) {
     const float4 v4 = ((const float4 *)row)[i];
     float e[4] = {v4.x, v4.y, v4.z, v4.w};
-    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = w4;
-    if (gw) {
+    float4 w4 = w0, b4 = b0;
+    if (gw && i != (int)threadIdx.x) {
       w4 = ((const float4 *)gw)[i];
       b4 = ((const float4 *)gb)[i];
     }

@@ -351,6 +351,8 @@ int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s) {
 // chain over the keys, one chain per output element.
 constexpr int ATT_THREADS = 1024;
 constexpr int ATT_WAVES = ATT_THREADS / 64;
+constexpr int ATT_KB = 4;   // keys per wave per load group
+constexpr int ATT_DPL = 4;  // max head-dim elements per lane (d <= 256)
 
 __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -389,29 +391,51 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   }
   __syncthreads();
   for (int i = tid; i < d; i += ATT_THREADS) A.kc[(size_t)n_past * E + h * d + i] = kh[i];
-  // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale
+  // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale.
+  // Each wave takes keys in groups of ATT_KB and loads the whole group before reducing, so
+  // the cache reads of a group overlap (one wave per key would pay the latency per key).
   float mx = -INFINITY;
-  for (int k = wid; k < nk; k += ATT_WAVES) {
-    const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
-    double t = 0.0, ta = 0.0;
-    for (int i = lane; i < d; i += 64) {
-      const double p = (double)(kr[i] * qh[i]);
-      t += p;
-      ta += fabs(p);
+  for (int k0 = wid * ATT_KB; k0 < nk; k0 += ATT_WAVES * ATT_KB) {
+    float kv[ATT_KB][ATT_DPL];
+#pragma unroll
+    for (int j = 0; j < ATT_KB; ++j) {
+      const int k = min(k0 + j, nk - 1);
+      const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
+#pragma unroll
+      for (int e = 0; e < ATT_DPL; ++e) {
+        const int i = lane + 64 * e;
+        kv[j][e] = i < d ? kr[i] : 0.0f;
+      }
     }
-    t = wave_sum_d(t);
-    ta = wave_sum_d(ta);
-    const double bnd = 2.0 * d * 0x1.0p-53 * ta;
-    float sc = (float)(t - bnd);
-    if (sc != (float)(t + bnd)) {  // wave-uniform: redo this key in the reference order
-      double acc = 0.0;
-      if (lane == 0)
-        for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
-      sc = (float)__shfl(acc, 0, 64);
+#pragma unroll
+    for (int j = 0; j < ATT_KB; ++j) {
+      const int k = k0 + j;
+      if (k >= nk) break;  // wave-uniform
+      double t = 0.0, ta = 0.0;
+#pragma unroll
+      for (int e = 0; e < ATT_DPL; ++e) {
+        const int i = lane + 64 * e;
+        if (i < d) {
+          const double p = (double)(kv[j][e] * qh[i]);
+          t += p;
+          ta += fabs(p);
+        }
+      }
+      t = wave_sum_d(t);
+      ta = wave_sum_d(ta);
+      const double bnd = 2.0 * d * 0x1.0p-53 * ta;
+      float sc = (float)(t - bnd);
+      if (sc != (float)(t + bnd)) {  // wave-uniform: redo this key in the reference order
+        const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
+        double acc = 0.0;
+        if (lane == 0)
+          for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
+        sc = (float)__shfl(acc, 0, 64);
+      }
+      sc = sc * A.scale;
+      if (lane == 0) pr[k] = sc;
+      mx = mx > sc ? mx : sc;
     }
-    sc = sc * A.scale;
-    if (lane == 0) pr[k] = sc;
-    mx = mx > sc ? mx : sc;
   }
   // max, exp via table, exact double sum (fp16 values: any order), 1/sum
   mx = wave_max_f(mx);
@@ -461,7 +485,10 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
 }
 
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s) {
-  if (A.d % 32 != 0) { set_error("attention: head dim must be a multiple of 32"); return VSIM_EINVAL; }
+  if (A.d % 32 != 0 || A.d > 64 * ATT_DPL) {
+    set_error("attention: head dim must be a multiple of 32, at most 256");
+    return VSIM_EINVAL;
+  }
   const size_t smem = (size_t)(2 * A.d + n_ctx) * sizeof(float);
   hipLaunchKernelGGL(k_attn_decode, dim3(A.H), dim3(ATT_THREADS), smem, s, A);
   VSIM_HIP(hipGetLastError());
