@@ -36,6 +36,31 @@ from vsim_amd import modelgen as mg  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s measured copy
 PROMPT = [50278, 12092, 2, 0, 50281]
+GEMV_KERNELS = ("k_gemv_chain", "k_gemv_fast")  # name prefixes of the Q4_0 GEMV launches
+# HBM traffic of the GEMV launches, from a separate `rocprofv3 --pmc FETCH_SIZE` pass of this
+# bench (tools/profile_round.sh) committed under profiles/; FETCH_SIZE is in KiB and reads
+# half of the bytes of a 16-byte-per-lane streaming read on gfx950 (MI355X_MICROARCH.md,
+# HBM section), so it is doubled.
+def pmc_file():
+    """The newest profiles/rNN_pmc_fetch_exact.csv (tools/profile_round.sh), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch_exact.csv")))
+    return files[-1] if files else None
+
+
+def pmc_traffic_per_launch(path=None):
+    """Mean corrected FETCH_SIZE bytes per GEMV launch, or None when no PMC pass is committed."""
+    import csv
+    path = path or pmc_file()
+    if not path or not os.path.exists(path):
+        return None
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name", "")
+            if r.get("Counter_Name") == "FETCH_SIZE" and any(k in name for k in GEMV_KERNELS):
+                vals.append(float(r["Counter_Value"]) * 1024.0 * 2.0)
+    return sum(vals) / len(vals) if vals else None
 
 
 def q4_weight_bytes(arch: str, hp: mg.HParams) -> float:
@@ -78,6 +103,38 @@ def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12):
     }
 
 
+def fast_companion(model, n_past, tok, steps):
+    """The integer-dot fast mode on the same weights: throughput, and the one-step logits error
+    against exact mode (each step is evaluated in both modes from the same exact KV cache;
+    over many steps the error compounds through the 4-bit activation re-quantization, see
+    tools/mode_drift.py), so it is a reported companion, not the headline value."""
+    rel, agree = [], 0
+    for i in range(4):
+        model.set_mode(hip.MODE_FAST)
+        lf = model.eval(n_past + i, [tok])
+        model.set_mode(hip.MODE_EXACT)
+        le = model.eval(n_past + i, [tok])
+        rel.append(float(np.max(np.abs(lf - le)) / np.max(np.abs(le))))
+        agree += int(np.argmax(lf) == np.argmax(le))
+        tok = int(np.argmax(le))
+    n_past += 4
+    model.set_mode(hip.MODE_FAST)
+    for i in range(4):
+        tok = int(np.argmax(model.eval(n_past + i, [tok])))
+    n_past += 4
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tok = int(np.argmax(model.eval(n_past + i, [tok])))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    model.set_mode(hip.MODE_EXACT)
+    return {"value": round(steps / dt, 3), "unit": "tokens/s", "steps": steps,
+            "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": agree / len(rel),
+            "parity": "not bit-exact; drifts across steps (tools/mode_drift.py)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +146,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-fast", action="store_true", help="skip the fast-mode companion measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,7 +161,7 @@ def main():
 
     arch_s, hp = mg.CONFIGS[args.config]
     arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
-    n_ctx = max(512, len(PROMPT) + args.warmup + 2 * args.steps + 8)
+    n_ctx = max(512, len(PROMPT) + args.warmup + 2 * args.steps + 96)
     model = hip.Model.create(arch, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
                                         n_layer=hp.n_layer, n_rot=hp.n_rot,
                                         use_parallel_residual=hp.use_parallel_residual),
@@ -157,12 +215,17 @@ def main():
             avg_ms = prof["gemv_ms"] / prof["gemv_launches"]
             bytes_per_launch = prof["gemv_bytes"] / prof["gemv_launches"]
             achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+            traffic = pmc_traffic_per_launch() if args.mode == "exact" and args.config == "gpt-j-6B" else None
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                        "kernel": "k_gemv_exact" if args.mode == "exact" else "k_gemv_fast",
+                        "frac": round(achieved / PEAK_HBM_GBS, 4),
+                        "traffic": round(traffic) if traffic else None,
+                        "kernel": "k_gemv_chain*" if args.mode == "exact" else "k_gemv_fast*",
                         "bytes_per_launch": round(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 3),
                         "launches": prof["gemv_launches"],
-                        "gemv_share_of_step": round(prof["gemv_ms"] / 1e3 / prof_wall, 4)}
+                        "gemv_share_of_step": round(prof["gemv_ms"] / 1e3 / prof_wall, 4),
+                        "note": ("exact mode is bound by the reference's sequential fp32 add chain per row "
+                                 "(K/2 dependent adds), not by HBM: see DESIGN.md 'chain floor'")
+                        if args.mode == "exact" else None}
 
     tokens_total = args.steps * world
     value = tokens_total / elapsed
@@ -190,6 +253,8 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_fast and args.mode == "exact":
+        line["fast_mode"] = fast_companion(model, n_past, tok, min(args.steps, 64))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(arch_s, hp)
     model.close()
