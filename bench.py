@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 from vsim_amd import hip  # noqa: E402
 from vsim_amd import modelgen as mg  # noqa: E402
+from vsim_amd import pipeline  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s measured copy
 PROMPT = [50278, 12092, 2, 0, 50281]
@@ -135,6 +136,93 @@ def fast_companion(model, n_past, tok, steps):
             "parity": "not bit-exact; drifts across steps (tools/mode_drift.py)"}
 
 
+def run_pipeline(args, world, rank, dev, dist):
+    """Layer split: rank r owns a contiguous layer range (rank 0 also the
+    embedding, the last rank ln_f + lm_head).  Per decode token the residual row [1][E] goes
+    rank r -> r+1 (one RCCL send/recv over xGMI per boundary) and the greedy token goes back
+    from the last rank to rank 0.  One token stream passes every stage in turn, so the value
+    is that stream's tokens/s (strong scaling: the work per token is fixed)."""
+    import torch
+    arch_s, hp = mg.CONFIGS[args.config]
+    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    L = hp.n_layer
+    per = (L + world - 1) // world
+    l0, l1 = pipeline.layer_range(L, world, rank)
+    n_ctx = max(512, len(PROMPT) + args.warmup + args.steps + 16)
+    hpd = dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head, n_layer=L, n_rot=hp.n_rot,
+               use_parallel_residual=hp.use_parallel_residual)
+    model = hip.Model.create(arch, hpd, n_ctx=n_ctx, device=dev, layer_begin=l0, layer_end=l1)
+    model.randomize(seed=1234 + rank, std=0.02)
+    model.set_mode(hip.MODE_EXACT if args.mode == "exact" else hip.MODE_FAST)
+    model.set_graph(not args.no_graph)
+    E = hp.n_embd
+    host = args.dist_backend == "gloo"
+    rbuf = torch.empty((len(PROMPT), E), dtype=torch.float32, device="cuda")
+    tokt = torch.zeros(1, dtype=torch.int64, device="cpu" if host else "cuda")
+
+    def send(t, dst):
+        dist.send(t.cpu() if host else t, dst=dst)
+
+    def recv(t, src):
+        if host:
+            c = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(c, src=src)
+            t.copy_(c)
+        else:
+            dist.recv(t, src=src)
+        torch.cuda.current_stream().synchronize()
+
+    def stage(n_past, ids, resid_in, resid_out):
+        return model.eval(n_past, ids, resid_in=resid_in, resid_out=resid_out)
+
+    def token_step(n_past, ids):
+        return pipeline.pipeline_step(rank, world, n_past, ids, stage, send, recv, rbuf[:len(ids)], tokt)
+
+    n_past = 0
+    tok = token_step(0, PROMPT)
+    n_past = len(PROMPT)
+    for _ in range(args.warmup):
+        tok = token_step(n_past, [tok])
+        n_past += 1
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tok = token_step(n_past, [tok])
+        n_past += 1
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = args.steps / elapsed
+    bw = q4_weight_bytes(arch_s, hp)
+    line = {
+        "metric": "decode tokens/sec GPT-J-6B Q4_0 @1 GPU; achieved HBM GB/s vs peak",
+        "value": round(value, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32 (Q4_0 x Q4_0 operands)",
+        "data": "synthetic (random-init weights of the config's shapes, drawn on device)",
+        "config": {"workload": f"{args.config} Q4_0 decode, layers split over {world} rank(s), "
+                               f"{args.steps} timed tokens after a 5-token prompt + {args.warmup} warm-up",
+                   "mode": args.mode, "n_ctx": n_ctx, "parallelism": f"pipeline{world}",
+                   "layers_per_rank": per, "send_bytes_per_token_per_boundary": 4 * E,
+                   "backend": args.dist_backend if world > 1 else None,
+                   "weight_bytes_per_token": bw, "weight_stream_GBps": round(bw * value / 1e9, 1)},
+        "roofline": None, "cpu_baseline": None,
+    }
+    model.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,17 +235,28 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-mode companion measurement")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="split the layers over the ranks (one residual send per stage boundary per token)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: host-staged sends, for rehearsing the pipeline with ranks sharing a GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+    if args.pipeline:
+        run_pipeline(args, world, rank, dev, dist)
+        return
 
     arch_s, hp = mg.CONFIGS[args.config]
     arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX

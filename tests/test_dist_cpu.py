@@ -1,0 +1,95 @@
+"""Multi-rank paths on CPU with gloo (no GPU): the layer-split protocol of vsim_amd/pipeline.py
+must give the same token stream as one rank running every layer, and the layer ranges must
+tile the model.  Each rank's stage is a deterministic float32 stand-in for its layers."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from vsim_amd import pipeline
+
+E, V, L = 16, 11, 7
+
+
+def _weights():
+    rng = np.random.default_rng(3)
+    return (rng.standard_normal((V, E)).astype(np.float32), rng.standard_normal((L, E, E)).astype(np.float32) * 0.3,
+            rng.standard_normal((V, E)).astype(np.float32))
+
+
+def _stage_fn(l0, l1, first, last, kv):
+    emb, layers, head = _weights()
+
+    def stage(n_past, ids, resid_in, resid_out):
+        x = emb[np.asarray(ids)] if first else resid_in.numpy().copy()
+        for l in range(l0, l1):
+            # position-dependent, cache-carrying stand-in for a layer (state per rank, like the KV cache)
+            kv.setdefault(l, []).append(x.sum())
+            x = np.tanh(x @ layers[l] + 0.01 * (n_past + len(kv[l])))
+        if last:
+            return (head @ x[-1]).astype(np.float32)
+        resid_out.copy_(torch.from_numpy(x.astype(np.float32)))
+        return None
+
+    return stage
+
+
+def _run(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    l0, l1 = pipeline.layer_range(L, world, rank)
+    stage = _stage_fn(l0, l1, rank == 0, rank == world - 1, {})
+    send = (lambda t, dst: dist.send(t, dst=dst)) if world > 1 else None
+    recv = (lambda t, src: dist.recv(t, src=src)) if world > 1 else None
+    prompt = [1, 4, 2]
+    resid = torch.zeros((len(prompt), E), dtype=torch.float32)
+    tok = torch.zeros(1, dtype=torch.int64)
+    toks = [pipeline.pipeline_step(rank, world, 0, prompt, stage, send, recv, resid, tok)]
+    n_past = len(prompt)
+    for _ in range(6):
+        toks.append(pipeline.pipeline_step(rank, world, n_past, [toks[-1]], stage, send, recv, resid[:1], tok))
+        n_past += 1
+    if rank == 0:
+        out.put(toks)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _stream(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    toks = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return toks
+
+
+def test_layer_ranges_tile_the_model():
+    for world in (1, 2, 3, 4, 7):
+        spans = [pipeline.layer_range(L, world, r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == L
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    with pytest.raises(ValueError):
+        pipeline.layer_range(L, 8, 7)  # 8 ranks for 7 layers: the last rank would be empty
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipeline_matches_single_rank(world):
+    assert _stream(world) == _stream(1)

@@ -1,0 +1,56 @@
+"""Layer-split decode protocol shared by bench.py and the CPU tests.
+
+Rank r owns a contiguous layer range; rank 0 also owns the token embedding and the last rank
+ln_f + lm_head (vsim.cpp:470-747 split at layer boundaries; with the parallel residual only
+the residual row inpL crosses a boundary).  Per eval:
+
+    rank 0:      resid = stage(n_past, tokens)            -> send resid to rank 1
+    rank 0<r<G-1: recv resid from r-1; resid = stage(...) -> send to r+1
+    rank G-1:    recv resid; logits = stage(...); token = argmax(logits) -> send to rank 0
+
+so one residual send per boundary per eval plus the sampled token back to rank 0 (the
+reference's loop feeds the sampled token into the next eval, vsim.cpp:860-891).
+"""
+from __future__ import annotations
+
+from typing import Callable, Sequence
+
+import numpy as np
+
+
+def layer_range(n_layer: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous split, ceil(L/G) layers per rank (the last ranks may hold fewer)."""
+    per = (n_layer + world - 1) // world
+    l0, l1 = min(n_layer, rank * per), min(n_layer, (rank + 1) * per)
+    if l1 <= l0:
+        raise ValueError(f"{world} ranks for {n_layer} layers leaves rank {rank} without layers")
+    return l0, l1
+
+
+def pipeline_step(rank: int, world: int, n_past: int, ids: Sequence[int],
+                  stage: Callable, send: Callable, recv: Callable, resid, tok) -> int:
+    """One eval of `ids` through every stage; returns the greedy next token on every rank
+    that takes part in the token hand-back (rank 0 and the last rank).
+
+    stage(n_past, ids, resid_in, resid_out) runs this rank's layers: ids on rank 0 (resid_in
+    None), resid_in otherwise; it fills resid_out on every rank but the last and returns the
+    logits row on the last.  send(t, dst) / recv(t, src) move a tensor; `resid` is the
+    [len(ids)][E] residual buffer and `tok` a 1-element integer tensor."""
+    first, last = rank == 0, rank == world - 1
+    if world == 1:
+        return int(np.argmax(stage(n_past, ids, None, None)))
+    if first:
+        stage(n_past, ids, None, resid)
+        send(resid, rank + 1)
+    else:
+        recv(resid, rank - 1)
+        out = stage(n_past, None, resid, None if last else resid)
+        if not last:
+            send(resid, rank + 1)
+        else:
+            tok[0] = int(np.argmax(out))
+    if last:
+        send(tok, 0)
+    if first:
+        recv(tok, world - 1)
+    return int(tok[0])
