@@ -24,6 +24,7 @@
 // Epilogues: plain store (+bias), and fc_in's bias + GELU table + re-quantization of the
 // 64 outputs into two blocks of the next product's Q4_0 activation (ggml.c:5024-5041).
 #include <cstdlib>
+#include <cstring>
 
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
@@ -464,7 +465,8 @@ __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
 template <int DBG>
 static void chain_launch_t(int grid, const GemvBatch &B, hipStream_t s) {
   // (CB = 4 at two workgroups per CU measured slower than CB = 8 at one: the producers'
-  // VALU issue per CU, not the grid's rounds, bounds the large batches)
+  // VALU issue per CU, not the grid's rounds, bounds the large batches.  Replacing the
+  // per-chunk barriers by LDS full/free counters was bit-exact but 10-20% slower.)
   hipLaunchKernelGGL((k_gemv_chain<DBG, 8>), dim3(grid), dim3(64 * 9), 0, s, B);
 }
 
