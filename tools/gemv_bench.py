@@ -67,7 +67,7 @@ def main():
             chain = K / 2 * 7.8 / 2.4e3  # us at 7.8 cycles per dependent add (measured), 2.4 GHz
             print(f"{name:16s} M={M:6d} K={K:6d} {'exact' if mode == 0 else 'fast ':5s} {us:9.2f} us "
                   f"{gbs:8.1f} GB/s  (chain floor {chain:.1f} us)", flush=True)
-            if mode == hip.MODE_EXACT and os.environ.get("VSIM_CHAIN_DBG") == "8":
+            if mode == hip.MODE_EXACT and int(os.environ.get("VSIM_CHAIN_DBG", "0")) & 8:
                 import ctypes
                 buf = (ctypes.c_ulonglong * 64)()
                 L.vsim_debug_chain_prof(buf)

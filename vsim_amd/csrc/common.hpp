@@ -85,17 +85,6 @@ struct LnQuantJob {
   float *jout;
 };
 
-// Rows [32t, 32t+32) of the out-projection (a) and of fc_out (b) in one workgroup, epilogue
-// inpL[row] = inpL[row] + ((a + bias_a) + (b + bias_b))  (vsim.cpp:694-695).
-struct DualJob {
-  W4 a, b;
-  const float *xda, *xdb;        // exact operands
-  const uint8_t *xqa, *xqb;      // fast operands (nibbles)
-  const float *xdda, *xddb;      // fast operands (scales)
-  const float *bias_a, *bias_b;  // bias_a may be NULL (GPT-J out_proj has none)
-  float *inpL;
-};
-
 struct AttnJob {
   const float *q, *k, *v;  // new rows [E] (Q, K, V after bias)
   float *kc, *vc;          // this layer's cache, [n_ctx][E]
@@ -114,7 +103,6 @@ int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream
 int launch_residual_join(const float *x, const float *a, const float *ab, const float *f, const float *fb, float *out,
                          int n, hipStream_t s);
 int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s);
-int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s);
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s);
 // exact-mode chain GEMV (gemv_chain.hip): a batch of jobs with the GemvBatch epilogues
 int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s);

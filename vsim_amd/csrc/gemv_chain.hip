@@ -164,13 +164,13 @@ __global__ void __launch_bounds__(64 * (1 + CB), 2) k_gemv_chain(GemvBatch B) {
       }
     };
     int ps = 0;  // P ring slot of chunk k
-    // one set of 32 SGPRs for the factors: chunk k+1's are loaded after chunk k's terms are
-    // done (their latency falls into the barrier wait; a second set costs the compiler
-    // enough SGPRs to force mid-step waits)
-    auto step = [&](int k, f32x2 *x, const uint4 &qc, float dqc, uint4 &qn, float &dqn) {
+    // two sets of 32 SGPRs for the factors: chunk k+1's load at the top of step k, so their
+    // latency falls into chunk k's compute instead of the barrier
+    auto step = [&](int k, const f32x2 *x, const uint4 &qc, float dqc, uint4 &qn, float &dqn, f32x2 *xn) {
       stamp(-1);
       rslot = rslot == CH_RAW - 1 ? 0 : rslot + 1;
       ldraw(rslot, qn, dqn);
+      ldx(k + 1, xn);
       if (!(DBG & 4)) dma(k + CH_DEPTH, dslot);
       dslot = dslot == CH_RAW - 1 ? 0 : dslot + 1;
       __builtin_amdgcn_sched_barrier(0);
@@ -189,7 +189,6 @@ __global__ void __launch_bounds__(64 * (1 + CB), 2) k_gemv_chain(GemvBatch B) {
       }
       ps = ps == CH_RING - 1 ? 0 : ps + 1;
       __builtin_amdgcn_sched_barrier(0);
-      ldx(k + 1, x);
       stamp(1);
       __builtin_amdgcn_s_waitcnt(WAIT_VM_DEPTH);  // this wave's DMA of chunk k+2 landed
       stamp(2);
@@ -199,17 +198,19 @@ __global__ void __launch_bounds__(64 * (1 + CB), 2) k_gemv_chain(GemvBatch B) {
 #pragma unroll
     for (int c = 0; c < CH_DEPTH; ++c) dma(c, c);
     dslot = CH_DEPTH % CH_RAW;
-    f32x2 xs[16];
+    f32x2 xa[16], xb[16];
     uint4 qa, qb;
     float da, db;
-    ldx(0, xs);
+    ldx(0, xa);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("" ::"s"(xa[i].x), "s"(xa[i].y));  // loaded before the loop
     __builtin_amdgcn_s_waitcnt(WAIT_VM_DEPTH);  // chunks 0 and 1 landed
     __syncthreads();
     ldraw(0, qa, da);
     __syncthreads();  // (second prologue barrier: the reads above are retired here)
     for (int k = 0; k < nit; k += 2) {
-      step(k, xs, qa, da, qb, db);
-      step(k + 1, xs, qb, db, qa, da);
+      step(k, xa, qa, da, qb, db, xb);
+      step(k + 1, xb, qb, db, qa, da, xa);
     }
     if (prof && lane == 0) {
       for (int i = 0; i < 4; ++i) g_chain_prof[16 + 4 * p + i] = pt[i];
@@ -513,6 +514,7 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     case 4: chain_launch_t<4>(groups, B, s); break;
     case 5: chain_launch_t<5>(groups, B, s); break;
     case 7: chain_launch_t<7>(groups, B, s); break;
+    case 10: chain_launch_t<10>(groups, B, s); break;
     case 12: chain_launch_t<12>(groups, B, s); break;
     case 8: chain_launch_t<8>(groups, B, s); break;
     default: chain_launch_t<0>(groups, B, s); break;

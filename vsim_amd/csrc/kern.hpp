@@ -53,22 +53,7 @@ __device__ __forceinline__ void pair_terms4(uint32_t w, float d0, const float *x
   }
 }
 
-// The same terms with each pair's two products packed together, {f0, f1} * {x[2k], x[2k+1]}:
-// the activation factors are used as adjacent (SGPR) pairs, no operand shuffles.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void pair_terms4_pk(uint32_t w, float d0, const f32x2 *x4, float *p4) {
-  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    f32x2 n;
-    n.x = __uint_as_float(__builtin_amdgcn_perm(0x4B4B4B4Bu, lo, 0x040C0C00u | k));
-    n.y = __uint_as_float(__builtin_amdgcn_perm(0x4B4B4B4Bu, hi, 0x040C0C00u | k));
-    n = n - 8388616.0f;
-    const f32x2 f = d0 * n;
-    const f32x2 t = f * x4[k];
-    p4[k] = t.x + t.y;
-  }
-}
 
 // v_cvt_f32_ubyteK: byte K of a word as float, one instruction (left to itself the compiler
 // extracts each byte first)
@@ -102,24 +87,6 @@ __device__ __forceinline__ void pair_terms4_fma(uint32_t w, f32x2 d2, f32x2 m2, 
   term(std::integral_constant<int, 1>{});
   term(std::integral_constant<int, 2>{});
   term(std::integral_constant<int, 3>{});
-}
-
-// Consumer step: add one full chunk of pairs into the chain.  All LDS reads are issued
-// before the first add (the hardware keeps up to 15 in flight), so the dependent add
-// chain does not stall on each read's latency.
-template <int CP>
-__device__ __forceinline__ float chain_chunk(const float *pr, float s) {
-  float4 v[CP / 4];
-#pragma unroll
-  for (int j = 0; j < CP / 4; ++j) v[j] = *(const float4 *)(pr + 4 * j);
-#pragma unroll
-  for (int j = 0; j < CP / 4; ++j) {
-    s = s + v[j].x;
-    s = s + v[j].y;
-    s = s + v[j].z;
-    s = s + v[j].w;
-  }
-  return s;
 }
 
 constexpr int NORM_THREADS = 256;

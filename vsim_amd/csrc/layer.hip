@@ -79,67 +79,6 @@ __device__ __forceinline__ void gemv_epilogue(const GemvJob &J, int t, float s, 
   }
 }
 
-// ------------------------------------------------------------------ 2. exact GEMV + epilogues
-// Producer/consumer over one 32-row tile (see k_gemv_exact_pc in ops_q4.hip for the
-// decomposition); this version adds the job epilogues.
-template <int C, int NPW>
-__global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_epi(GemvBatch B) {
-  constexpr int CP = C * 16;
-  constexpr int LD = CP + 4;
-  __shared__ __attribute__((aligned(16))) float P[2][T32 * LD];
-  int t = blockIdx.x, ji = 0;
-  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
-  const GemvJob &J = B.j[ji];
-  const int nb = J.w.nb();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nchunks = (nb + C - 1) / C;
-  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
-  const float *dd = J.w.d + (size_t)t * nb * T32;
-  float s = 0.0f;
-  for (int c = 0; c <= nchunks; ++c) {
-    if (wave > 0 && c < nchunks) {
-      float *Ps = P[c & 1];
-      for (int i = (wave - 1) * 64 + lane; i < T32 * C; i += NPW * 64) {
-        const int r = i & (T32 - 1), b = i / T32;
-        const int blk = c * C + b;
-        if (blk < nb) {
-          const size_t o = (size_t)blk * T32 + r;
-          const float d0 = dd[o];
-          const uint4 q = *(const uint4 *)(qs + o * 16);
-          const float4 *xv = (const float4 *)(J.xd + (size_t)blk * QK);
-          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-          float4 *dst = (float4 *)(Ps + r * LD + b * 16);
-#pragma unroll
-          for (int wv = 0; wv < 4; ++wv) {
-            const float4 a = xv[2 * wv], bb = xv[2 * wv + 1];
-            const float x8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
-            float p4[4];
-            pair_terms4(qw[wv], d0, x8, p4);
-            dst[wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
-          }
-        }
-      }
-    }
-    if (wave == 0 && c > 0 && lane < T32) {
-      const float *pr = P[(c - 1) & 1] + lane * LD;
-      const int np = min(C, nb - (c - 1) * C) * 16;
-      if (np == CP) {
-        s = chain_chunk<CP>(pr, s);
-      } else {
-        for (int j = 0; j < np; j += 4) {
-          const float4 v = *(const float4 *)(pr + j);
-          s = s + v.x;
-          s = s + v.y;
-          s = s + v.z;
-          s = s + v.w;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (wave == 0) gemv_epilogue(J, t, s, lane);
-}
-
 // ------------------------------------------------------------------ fast GEMV + epilogues
 constexpr int FW = 8;  // waves per workgroup of the fast kernels
 __global__ void __launch_bounds__(64 * FW) k_gemv_fast_epi(GemvBatch B) {
@@ -176,168 +115,11 @@ __global__ void __launch_bounds__(64 * FW) k_gemv_fast_epi(GemvBatch B) {
   }
 }
 
-static bool legacy_exact() {
-  static const bool v = getenv("VSIM_LEGACY_EXACT") != nullptr;
-  return v;
-}
-
 int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s) {
   int tiles = 0;
   for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
-  if (mode == VSIM_MODE_EXACT && !legacy_exact()) return launch_gemv_chain_batch(B, s);
-  if (mode == VSIM_MODE_EXACT)
-    hipLaunchKernelGGL((k_gemv_exact_epi<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B);
-  else
-    hipLaunchKernelGGL(k_gemv_fast_epi, dim3(tiles), dim3(64 * FW), 0, s, B);
-  VSIM_HIP(hipGetLastError());
-  return VSIM_OK;
-}
-
-// ------------------------------------------------------------------ 4. dual GEMV + residual
-// Rows [32t, 32t+32) of the out-projection (A: K = E, input = attention output) and of
-// fc_out (B: K = 4E, input = quantized GELU output) in one workgroup; the consumer lanes run
-// both chains interleaved (two independent dependent chains share the add latency), then
-// inpL[row] = inpL[row] + ((A + biasA) + (B + biasB)).
-template <int C>
-__device__ __forceinline__ void produce_chunk(const W4 &w, int t, const float *xd, int c, float *Ps, int item, int LD) {
-  const int nb = w.nb();
-  const int r = item & (T32 - 1), b = item / T32;
-  const int blk = c * C + b;
-  if (blk >= nb) return;
-  const size_t o = ((size_t)t * nb + blk) * T32 + r;
-  const float d0 = w.d[o];
-  const uint4 q = *(const uint4 *)(w.qs + o * 16);
-  const float4 *xv = (const float4 *)(xd + (size_t)blk * QK);
-  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-  float4 *dst = (float4 *)(Ps + r * LD + b * 16);
-#pragma unroll
-  for (int wv = 0; wv < 4; ++wv) {
-    const float4 a = xv[2 * wv], bb = xv[2 * wv + 1];
-    const float x8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
-    float p4[4];
-    pair_terms4(qw[wv], d0, x8, p4);
-    dst[wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
-  }
-}
-
-template <int C, int NPW>
-__global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_dual(DualJob D) {
-  constexpr int CP = C * 16;
-  constexpr int LD = CP + 4;
-  __shared__ __attribute__((aligned(16))) float PA[2][T32 * LD];
-  __shared__ __attribute__((aligned(16))) float PB[2][T32 * LD];
-  const int t = blockIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nca = (D.a.nb() + C - 1) / C, ncb = (D.b.nb() + C - 1) / C;
-  const int nch = max(nca, ncb);
-  float sa = 0.0f, sb = 0.0f;
-  for (int c = 0; c <= nch; ++c) {
-    if (wave > 0 && c < nch) {
-      for (int i = (wave - 1) * 64 + lane; i < 2 * T32 * C; i += NPW * 64) {
-        if (i < T32 * C) {
-          if (c < nca) produce_chunk<C>(D.a, t, D.xda, c, PA[c & 1], i, LD);
-        } else if (c < ncb) {
-          produce_chunk<C>(D.b, t, D.xdb, c, PB[c & 1], i - T32 * C, LD);
-        }
-      }
-    }
-    if (wave == 0 && c > 0 && lane < T32) {
-      const int cc = c - 1;
-      const float *pa = PA[cc & 1] + lane * LD;
-      const float *pb = PB[cc & 1] + lane * LD;
-      const int npa = cc < nca ? min(C, D.a.nb() - cc * C) * 16 : 0;
-      const int npb = cc < ncb ? min(C, D.b.nb() - cc * C) * 16 : 0;
-      if (npa == CP && npb == CP) {
-        float4 va[CP / 4], vb[CP / 4];
-#pragma unroll
-        for (int j = 0; j < CP / 4; ++j) {
-          va[j] = *(const float4 *)(pa + 4 * j);
-          vb[j] = *(const float4 *)(pb + 4 * j);
-        }
-#pragma unroll
-        for (int j = 0; j < CP / 4; ++j) {
-          sa = sa + va[j].x; sb = sb + vb[j].x;
-          sa = sa + va[j].y; sb = sb + vb[j].y;
-          sa = sa + va[j].z; sb = sb + vb[j].z;
-          sa = sa + va[j].w; sb = sb + vb[j].w;
-        }
-      } else {
-        for (int j = 0; j < npa; j += 4) {
-          const float4 v = *(const float4 *)(pa + j);
-          sa = sa + v.x; sa = sa + v.y; sa = sa + v.z; sa = sa + v.w;
-        }
-        if (npb == CP) {
-          sb = chain_chunk<CP>(pb, sb);
-        } else {
-          for (int j = 0; j < npb; j += 4) {
-            const float4 v = *(const float4 *)(pb + j);
-            sb = sb + v.x; sb = sb + v.y; sb = sb + v.z; sb = sb + v.w;
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (wave == 0 && lane < T32) {
-    const int row = t * T32 + lane;
-    if (row < D.a.rows) {
-      const float attn = D.bias_a ? sa + D.bias_a[row] : sa;
-      const float ff = sb + D.bias_b[row];
-      D.inpL[row] = D.inpL[row] + (attn + ff);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(64 * FW) k_gemv_fast_dual(DualJob D) {
-  __shared__ float part[2][FW * 2][T32];
-  const int t = blockIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & (T32 - 1), h = lane >> 5;
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const W4 &w = m == 0 ? D.a : D.b;
-    const uint8_t *xq = m == 0 ? D.xqa : D.xqb;
-    const float *xdd = m == 0 ? D.xdda : D.xddb;
-    const int nb = w.nb();
-    const uint8_t *qs = w.qs + (size_t)t * nb * T32 * 16;
-    const float *dd = w.d + (size_t)t * nb * T32;
-    float acc = 0.0f;
-    for (int b = 2 * wave + h; b < nb; b += 2 * FW) {
-      const size_t o = (size_t)b * T32 + r;
-      const uint4 q = *(const uint4 *)(qs + o * 16);
-      const float d0 = dd[o];
-      const uint4 xv = *(const uint4 *)(xq + (size_t)b * 16);
-      int sd = __builtin_amdgcn_sdot8((int)(q.x ^ 0x88888888u), (int)(xv.x ^ 0x88888888u), 0, false);
-      sd = __builtin_amdgcn_sdot8((int)(q.y ^ 0x88888888u), (int)(xv.y ^ 0x88888888u), sd, false);
-      sd = __builtin_amdgcn_sdot8((int)(q.z ^ 0x88888888u), (int)(xv.z ^ 0x88888888u), sd, false);
-      sd = __builtin_amdgcn_sdot8((int)(q.w ^ 0x88888888u), (int)(xv.w ^ 0x88888888u), sd, false);
-      acc = __builtin_fmaf(d0 * xdd[b], (float)sd, acc);
-    }
-    part[m][2 * wave + h][r] = acc;
-  }
-  __syncthreads();
-  if (threadIdx.x < T32) {
-    float sa = 0.0f, sb = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2 * FW; ++i) {
-      sa += part[0][i][threadIdx.x];
-      sb += part[1][i][threadIdx.x];
-    }
-    const int row = t * T32 + threadIdx.x;
-    if (row < D.a.rows) {
-      const float attn = D.bias_a ? sa + D.bias_a[row] : sa;
-      const float ff = sb + D.bias_b[row];
-      D.inpL[row] = D.inpL[row] + (attn + ff);
-    }
-  }
-}
-
-int launch_gemv_dual(const DualJob &D, int mode, hipStream_t s) {
-  if (D.a.rows != D.b.rows) { set_error("dual gemv: row mismatch"); return VSIM_EINVAL; }
-  if (mode == VSIM_MODE_EXACT)
-    hipLaunchKernelGGL((k_gemv_exact_dual<4, 7>), dim3(D.a.tiles), dim3(64 * 8), 0, s, D);
-  else
-    hipLaunchKernelGGL(k_gemv_fast_dual, dim3(D.a.tiles), dim3(64 * FW), 0, s, D);
+  if (mode == VSIM_MODE_EXACT) return launch_gemv_chain_batch(B, s);  // gemv_chain.hip
+  hipLaunchKernelGGL(k_gemv_fast_epi, dim3(tiles), dim3(64 * FW), 0, s, B);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

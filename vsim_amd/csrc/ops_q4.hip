@@ -191,189 +191,6 @@ __global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__re
 // ------------------------------------------------------------------ activation quantize
 // (quantize_block: kern.hpp)
 
-// ------------------------------------------------------------------ exact GEMV (decode)
-// Producer/consumer over one 32-row tile and the whole K (the chain order forbids
-// splitting K).  Producer waves turn a chunk of C blocks x 32 rows into pair values
-// p[r][j] in LDS (all the VALU work, in parallel); the consumer wave adds them into the
-// 32 row chains in the reference order, one dependent add per pair, while the producers
-// fill the other LDS slot.  Layout [slot][row][pair] with a 4-float pad: producer
-// ds_write_b128 (8-lane groups on distinct 4-bank groups) and consumer ds_read_b128
-// (16-lane groups covering all 64 banks) are conflict-free.
-template <int C, int NPW, int DBG = 0>  // DBG (diagnostics only): 1 = no global loads, 2 = no producers
-__global__ void __launch_bounds__(64 * (1 + NPW)) k_gemv_exact_pc(GemvBatch B) {
-  constexpr int CP = C * 16;  // pairs per row per chunk
-  constexpr int LD = CP + 4;  // padded row stride (floats)
-  __shared__ __attribute__((aligned(16))) float P[2][T32 * LD];
-  int t = blockIdx.x, ji = 0;
-  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
-  const GemvJob J = B.j[ji];
-  const int nb = J.w.nb();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nchunks = (nb + C - 1) / C;
-  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
-  const float *dd = J.w.d + (size_t)t * nb * T32;
-  float s = 0.0f;
-  for (int c = 0; c <= nchunks; ++c) {
-    if (DBG != 2 && wave > 0 && c < nchunks) {
-      float *Ps = P[c & 1];
-      for (int i = (wave - 1) * 64 + lane; i < T32 * C; i += NPW * 64) {
-        const int r = i & (T32 - 1), b = i / T32;
-        const int blk = c * C + b;
-        if (blk < nb) {
-          const size_t o = (size_t)blk * T32 + r;
-          const float d0 = DBG == 1 ? (float)o * 1e-6f : dd[o];
-          const uint4 q = DBG == 1 ? make_uint4(o, o * 3, o * 5, o * 7) : *(const uint4 *)(qs + o * 16);
-          const float4 *xv = (const float4 *)(J.xd + (size_t)(DBG == 1 ? 0 : blk) * QK);
-          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-          float4 *dst = (float4 *)(Ps + r * LD + b * 16);
-#pragma unroll
-          for (int wv = 0; wv < 4; ++wv) {
-            const float4 a = xv[2 * wv], bb = xv[2 * wv + 1];
-            const float x8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
-            float p4[4];
-            pair_terms4(qw[wv], d0, x8, p4);
-            dst[wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
-          }
-        }
-      }
-    }
-    if (wave == 0 && c > 0 && lane < T32) {
-      const float *pr = P[(c - 1) & 1] + lane * LD;
-      const int np = min(C, nb - (c - 1) * C) * 16;
-      if (np == CP) {
-        s = chain_chunk<CP>(pr, s);
-      } else {
-        for (int j = 0; j < np; j += 4) {
-          const float4 v = *(const float4 *)(pr + j);
-          s = s + v.x;
-          s = s + v.y;
-          s = s + v.z;
-          s = s + v.w;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (wave == 0 && lane < T32) {
-    const int row = t * T32 + lane;
-    if (row < J.w.rows) J.y[row] = J.bias ? s + J.bias[row] : s;
-  }
-}
-
-// ------------------------------------------------------------------ exact GEMV v2
-// Same decomposition with a deep pipeline: producer wave w (1..NP) owns LDS slot w and
-// produces chunks w-1, w-1+NP, ...; it issues the loads of its next chunk before it
-// computes the current one, so NP chunks (NP*C blocks of 32 rows) are in flight to hide
-// HBM latency behind the consumer's dependent chain.  Hand-off through LDS flags:
-// ready[slot] = chunk+1 (producer, after its LDS writes), consumed = chunks done
-// (consumer).  Only waves of one workgroup talk, all resident, every wait is bounded by
-// progress the other side is guaranteed to make.
-template <int C, int NP>
-__global__ void __launch_bounds__(64 * (1 + NP)) k_gemv_exact_v2(GemvBatch B) {
-  constexpr int CP = C * 16;
-  constexpr int LD = CP + 4;
-  constexpr int ITEMS = T32 * C / 64;  // (row, block) items per producer lane per chunk
-  __shared__ __attribute__((aligned(16))) float P[NP][T32 * LD];
-  __shared__ int ready[NP];
-  __shared__ int consumed;
-  int t = blockIdx.x, ji = 0;
-  while (ji + 1 < B.nj && t >= B.j[ji].w.tiles) { t -= B.j[ji].w.tiles; ++ji; }
-  const GemvJob J = B.j[ji];
-  const int nb = J.w.nb();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nchunks = (nb + C - 1) / C;
-  const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16;
-  const float *dd = J.w.d + (size_t)t * nb * T32;
-  if (threadIdx.x < NP) ready[threadIdx.x] = 0;
-  if (threadIdx.x == 0) consumed = 0;
-  __syncthreads();
-  if (wave == 0) {
-    __builtin_amdgcn_s_setprio(3);
-    float s = 0.0f;
-    for (int c = 0; c < nchunks; ++c) {
-      const int slot = c % NP;
-      while (__hip_atomic_load(&ready[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1)
-        __builtin_amdgcn_s_sleep(0);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (lane < T32) {
-        const float *pr = P[slot] + lane * LD;
-        const int np = min(C, nb - c * C) * 16;
-        if (np == CP) {
-          s = chain_chunk<CP>(pr, s);
-        } else {
-          for (int j = 0; j < np; j += 4) {
-            const float4 v = *(const float4 *)(pr + j);
-            s = s + v.x;
-            s = s + v.y;
-            s = s + v.z;
-            s = s + v.w;
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&consumed, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (lane < T32) {
-      const int row = t * T32 + lane;
-      if (row < J.w.rows) J.y[row] = J.bias ? s + J.bias[row] : s;
-    }
-    return;
-  }
-  // producers
-  const int pw = wave - 1;
-  uint4 q[ITEMS];
-  float d0[ITEMS];
-  float4 xv[ITEMS][8];
-  auto load = [&](int c) {
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-      const int i = it * 64 + lane;
-      const int r = i & (T32 - 1), b = i / T32;
-      const int blk = min(c * C + b, nb - 1);  // clamp: tail items load a valid block, never stored
-      const size_t o = (size_t)blk * T32 + r;
-      d0[it] = dd[o];
-      q[it] = *(const uint4 *)(qs + o * 16);
-      const float4 *x = (const float4 *)(J.xd + (size_t)blk * QK);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) xv[it][k] = x[k];
-    }
-  };
-  if (pw < nchunks) load(pw);
-  for (int c = pw; c < nchunks; c += NP) {
-    // registers now hold chunk c; compute it after its slot is free
-    float4 pv[ITEMS][4];
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-      const uint32_t qw[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) {
-        const float x8[8] = {xv[it][2 * wv].x, xv[it][2 * wv].y, xv[it][2 * wv].z, xv[it][2 * wv].w,
-                             xv[it][2 * wv + 1].x, xv[it][2 * wv + 1].y, xv[it][2 * wv + 1].z, xv[it][2 * wv + 1].w};
-        float p4[4];
-        pair_terms4(qw[wv], d0[it], x8, p4);
-        pv[it][wv] = make_float4(p4[0], p4[1], p4[2], p4[3]);
-      }
-    }
-    if (c + NP < nchunks) load(c + NP);  // prefetch this wave's next chunk
-    while (__hip_atomic_load(&consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < c - NP + 1)
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    float *Ps = P[c % NP];
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-      const int i = it * 64 + lane;
-      const int r = i & (T32 - 1), b = i / T32;
-      if (c * C + b < nb) {
-        float4 *dst = (float4 *)(Ps + r * LD + b * 16);
-#pragma unroll
-        for (int wv = 0; wv < 4; ++wv) dst[wv] = pv[it][wv];
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(&ready[c % NP], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
 // ------------------------------------------------------------------ fast GEMV
 // HBM-streaming form of the same product: one 512-thread workgroup per 32-row tile, lane
 // (r, h) = (lane & 31, lane >> 5) of wave w streams blocks b = 2w + h, +16, ... (each
@@ -419,26 +236,7 @@ int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
   for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
   if (tiles == 0) return VSIM_OK;
   if (mode == VSIM_MODE_EXACT) {
-    static int variant = [] {
-      const char *e = getenv("VSIM_GEMV_PC");
-      return e ? atoi(e) : 0;
-    }();
-    if (variant == 0) return launch_gemv_chain_batch(B, s);  // gemv_chain.hip
-    switch (variant) {  // older producer/consumer kernels kept for A/B timing
-      case 1: hipLaunchKernelGGL((k_gemv_exact_pc<4, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
-      case 2: hipLaunchKernelGGL((k_gemv_exact_pc<16, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
-      case 3: hipLaunchKernelGGL((k_gemv_exact_pc<8, 3>), dim3(tiles), dim3(64 * 4), 0, s, B); break;
-      case 4: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      case 5: hipLaunchKernelGGL((k_gemv_exact_pc<16, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      case 6: hipLaunchKernelGGL((k_gemv_exact_v2<4, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      case 7: hipLaunchKernelGGL((k_gemv_exact_v2<2, 13>), dim3(tiles), dim3(64 * 14), 0, s, B); break;
-      case 8: hipLaunchKernelGGL((k_gemv_exact_v2<8, 3>), dim3(tiles), dim3(64 * 4), 0, s, B); break;
-      case 9: hipLaunchKernelGGL((k_gemv_exact_v2<2, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      case 10: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7, 1>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      case 11: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7, 2>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      case 12: hipLaunchKernelGGL((k_gemv_exact_pc<8, 7>), dim3(tiles), dim3(64 * 8), 0, s, B); break;
-      default: hipLaunchKernelGGL((k_gemv_exact_pc<8, 4>), dim3(tiles), dim3(64 * 5), 0, s, B); break;
-    }
+    return launch_gemv_chain_batch(B, s);  // gemv_chain.hip
   } else {
     hipLaunchKernelGGL(k_gemv_fast, dim3(tiles), dim3(64 * FAST_WAVES), 0, s, B);
   }
