@@ -177,13 +177,13 @@ __global__ void __launch_bounds__(64 * (1 + CB), 2) k_gemv_chain(GemvBatch B) {
       stamp(0);
       if (!(DBG & 2)) {
         const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
-        const f32x2 d2 = {dv, dv}, m2 = {-8.0f * dv, -8.0f * dv};
+        const f32x2 d2 = {512.0f * dv, 512.0f * dv}, m2 = {-8.0f * dv, -8.0f * dv};
         float *dst = &P[ps][lane * LD + o * 16];
         const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
 #pragma unroll
         for (int wv = 0; wv < 4; ++wv) {
           float p4[4];
-          pair_terms4_fma(qw[wv], d2, m2, x + 4 * wv, p4);
+          pair_terms4_x(qw[wv], d2, m2, x + 4 * wv, p4);
           *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
         }
       }
@@ -375,13 +375,13 @@ __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
       if (!(DBG & 4)) dma(k + C2_DEPTH);
       if (!(DBG & 2)) {
         const float dv = k * C2_CB + o < nb ? dqc : 0.0f;
-        const f32x2 d2 = {dv, dv}, m2 = {-8.0f * dv, -8.0f * dv};
+        const f32x2 d2 = {512.0f * dv, 512.0f * dv}, m2 = {-8.0f * dv, -8.0f * dv};
         float *dst = &P[ps][r * C2_LD + o * 16];
         const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
 #pragma unroll
         for (int wv = 0; wv < 4; ++wv) {
           float p4[4];
-          pair_terms4_fma(qw[wv], d2, m2, xc + 4 * wv, p4);
+          pair_terms4_x(qw[wv], d2, m2, xc + 4 * wv, p4);
           *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
         }
       }

@@ -7,6 +7,13 @@
 
 namespace vsim {
 
+// ------------------------------------------------------------------ activation factors
+// xd, the exact path's dequantized activation d*(q-8), is stored pair-interleaved: within
+// each group of four elements the middle two swap places, (x0, x2, x1, x3).  Two adjacent
+// floats then hold the same factor slot (first or second) of two consecutive byte pairs,
+// which is what one packed multiply needs (pair_terms4_x).
+__host__ __device__ constexpr int xd_slot(int l) { return (l & ~3) | ((l & 1) << 1) | ((l >> 1) & 1); }
+
 // ------------------------------------------------------------------ activation quantize
 // One thread per 32-block.  Bit-identical to quantize_row_q4_0: fp32 amax, d = amax/7
 // (correctly rounded division), id = 1/d, q = (int8)round(x*id) + 8 with round-half-
@@ -33,7 +40,7 @@ __device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, 
   if (xd_out) {
     float4 *o = (float4 *)xd_out;
 #pragma unroll
-    for (int i = 0; i < QK / 4; ++i) o[i] = make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
+    for (int i = 0; i < QK / 4; ++i) o[i] = make_float4(out[4 * i], out[4 * i + 2], out[4 * i + 1], out[4 * i + 3]);
   }
 }
 
@@ -87,6 +94,27 @@ __device__ __forceinline__ void pair_terms4_fma(uint32_t w, f32x2 d2, f32x2 m2, 
   term(std::integral_constant<int, 1>{});
   term(std::integral_constant<int, 2>{});
   term(std::integral_constant<int, 3>{});
+}
+
+// The four terms of a word with pairs packed across the two lanes of each vector op: byte k
+// of lo (hi) holds the first (second) nibble of pair k, and v_cvt_pk_f32_fp8 turns two of
+// those bytes into floats at once -- an e4m3 byte with value n in 0..15 decodes to exactly
+// n * 2^-9, so with d512 = 512*d0 the fma gives d0*(n-8) exactly as above.  xw holds the
+// pair-interleaved factors (xd_slot): xw[0] = {x0, x2} (first factors of pairs 0 and 1),
+// xw[1] = {x1, x3}, xw[2] = {x4, x6}, xw[3] = {x5, x7}.  Per word: 3 integer ops, 4
+// conversions, 4 fma, 4 mul, 2 add (all packed) for the reference's 4 x 7 scalar ops.
+__device__ __forceinline__ void pair_terms4_x(uint32_t w, f32x2 d512, f32x2 m2, const f32x2 *xw, float *p4) {
+  const int lo = (int)(w & 0x0F0F0F0Fu), hi = (int)((w >> 4) & 0x0F0F0F0Fu);
+  const f32x2 f01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, false), d512, m2);
+  const f32x2 g01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, false), d512, m2);
+  const f32x2 f23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, true), d512, m2);
+  const f32x2 g23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, true), d512, m2);
+  const f32x2 t01 = f01 * xw[0] + g01 * xw[1];
+  const f32x2 t23 = f23 * xw[2] + g23 * xw[3];
+  p4[0] = t01.x;
+  p4[1] = t01.y;
+  p4[2] = t23.x;
+  p4[3] = t23.y;
 }
 
 constexpr int NORM_THREADS = 256;
@@ -281,7 +309,7 @@ __device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_
   if (ok) {
     if ((l & 7) == 0) ((uint32_t *)qs_out)[l >> 3] = word;
     if (l == 0) *d_out = d;
-    xd_out[l] = d * (float)(q - 8);
+    xd_out[xd_slot(l)] = d * (float)(q - 8);
   }
 }
 
@@ -309,7 +337,7 @@ __device__ __forceinline__ void quantize_block_lanes(float v, int lane, uint8_t 
   if (lane < 32) {
     if ((lane & 7) == 0) ((uint32_t *)qs_out)[lane >> 3] = word;
     if (lane == 0) *d_out = d;
-    xd_out[lane] = d * (float)(q - 8);
+    xd_out[xd_slot(lane)] = d * (float)(q - 8);
   }
 }
 

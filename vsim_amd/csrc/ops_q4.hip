@@ -143,8 +143,8 @@ __global__ void k_q4_dequant(const uint8_t *__restrict__ qs, const float *__rest
 #pragma unroll
     for (int bj = 0; bj < 4; ++bj) {
       const uint32_t byte = (qw[wv] >> (8 * bj)) & 0xFF;
-      o[2 * (wv * 4 + bj)] = d * (float)((int)(byte & 0xF) - 8);
-      o[2 * (wv * 4 + bj) + 1] = d * (float)((int)(byte >> 4) - 8);
+      o[xd_slot(2 * (wv * 4 + bj))] = d * (float)((int)(byte & 0xF) - 8);
+      o[xd_slot(2 * (wv * 4 + bj) + 1)] = d * (float)((int)(byte >> 4) - 8);
     }
 }
 
@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__re
     for (int wv = 0; wv < 4; ++wv) {
       const float4 a = *(const float4 *)(xr + i * QK + wv * 8);
       const float4 b = *(const float4 *)(xr + i * QK + wv * 8 + 4);
-      const float x8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const float x8[8] = {a.x, a.z, a.y, a.w, b.x, b.z, b.y, b.w};  // pair-interleaved (xd_slot)
       float p4[4];
       pair_terms4(qw[wv], d0, x8, p4);
       acc = acc + p4[0];
