@@ -463,6 +463,166 @@ __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
   }
 }
 
+// ================================================================== 128-row variant
+// Two consumer waves (rows 0-63 and 64-127 of the workgroup, on SIMD0 and SIMD1) and 12
+// producer waves (three per SIMD: one wave alone issues VALU at ~1 per 5 cycles, three
+// share a SIMD at ~1 per 2).  A chunk is C3_CB = 6 blocks; producer p computes block p % 6
+// of row group p / 6.  With 128 rows in flight per CU a K = 4096 batch of up to 32768 rows
+// (Q, K, V and fc_in of GPT-J: 28672) is a single round of workgroups, each CU running two
+// chains at once instead of one.  The pair-term ring takes the whole LDS (3 x 128 rows x
+// 100 floats), so nibbles and scales come straight from global memory into a register ring
+// C3_PF chunks ahead (the compiler's own loads: its vmcnt bookkeeping waits only for the
+// oldest set) and the activation factors by scalar loads one chunk ahead, as in
+// k_gemv_chain.
+constexpr int C3_CB = 6, C3_CP = C3_CB * 16, C3_LD = C3_CP + 4, C3_NP = 2 * C3_CB;
+constexpr int C3_THREADS = 64 * (2 + C3_NP);
+constexpr int C3_RING = 3, C3_WIN = 8, C3_PF = 3;  // register ring: C3_PF + 1 sets
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+typedef const __attribute__((address_space(1))) float gfloat;
+
+template <int DBG>
+__global__ void __launch_bounds__(C3_THREADS, 1) k_gemv_chain2(GemvBatch B) {
+  __shared__ __attribute__((aligned(16))) float P[C3_RING][128 * C3_LD];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  int g = blockIdx.x, ji = 0;
+  while (ji < B.nj) {
+    const int ng = (B.j[ji].w.tiles + 3) / 4;
+    if (g < ng) break;
+    g -= ng;
+    ++ji;
+  }
+  if (ji >= B.nj) return;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  g = __builtin_amdgcn_readfirstlane(g);
+  const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + C3_CB - 1) / C3_CB;
+  // chunk k is produced in iteration k and added in k+2; a multiple of 4 for the producers'
+  // unrolled register rings
+  const int nit = (nch + 2 + 3) & ~3;
+
+  if (wave >= 2) {
+    // ------------------------------------------------------------- producer
+    const int p = wave - 2, o = p % C3_CB, rg = p / C3_CB;
+    const int h = lane >> 5, r = lane & 31;
+    const int tile = 4 * g + 2 * rg + h;
+    const bool tile_ok = tile < tiles;
+    const int tl = tile_ok ? tile : tiles - 1;  // absent tile: in-bounds loads, zero terms
+    const uint8_t *qs = B.j[ji].w.qs + ((size_t)tl * nb * T32 + r) * 16;
+    const float *dd = B.j[ji].w.d + (size_t)tl * nb * T32 + r;
+    const float *xg = B.j[ji].xd;
+    auto ld = [&](int c, u32x4 &qv, float &dv) {
+      const int b = min(c * C3_CB + o, nb - 1);
+      qv = __builtin_nontemporal_load((gu32x4 *)(qs + (size_t)b * (T32 * 16)));
+      dv = __builtin_nontemporal_load((gfloat *)(dd + (size_t)b * T32));
+    };
+    auto ldx = [&](int c, f32x2 *xv) {
+      const int b = min(c * C3_CB + o, nb - 1);
+      const sfloat *xp = (const sfloat *)(xg + (size_t)b * QK);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        xv[i].x = xp[2 * i];
+        xv[i].y = xp[2 * i + 1];
+      }
+    };
+    int ps = 0;
+    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
+      ld(k + C3_PF, qn, dqn);  // the set of chunk k-1, used in the previous step
+      ldx(k + 1, xn);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(DBG & 2)) {
+        const float dv = tile_ok && k * C3_CB + o < nb ? dqc : 0.0f;
+        // both halves of the broadcast pairs as real registers: with one half left undefined
+        // the allocator may overlay it on a register whose global load is still in flight,
+        // and the read of the pair then waits for that load
+        const float dl = 512.0f * dv, ml = -8.0f * dv;
+        float dh, mh;
+        asm("v_mov_b32 %0, %1" : "=v"(dh) : "v"(dl));
+        asm("v_mov_b32 %0, %1" : "=v"(mh) : "v"(ml));
+        const f32x2 d2 = {dl, dh}, m2 = {ml, mh};
+        float *dst = &P[ps][(rg * 64 + lane) * C3_LD + o * 16];
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) {
+          float p4[4];
+          pair_terms4_x(qc[wv], d2, m2, xc + 4 * wv, p4);
+          *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+        }
+      }
+      ps = ps == C3_RING - 1 ? 0 : ps + 1;
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+    };
+    u32x4 q0, q1, q2, q3;
+    float e0, e1, e2, e3;
+    ld(0, q0, e0);
+    ld(1, q1, e1);
+    ld(2, q2, e2);
+    f32x2 xa[16], xb[16];
+    ldx(0, xa);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("" ::"s"(xa[i].x), "s"(xa[i].y));  // loaded before the loop
+    static_assert(C3_PF == 3, "register ring unrolled for 4 sets");
+    for (int k = 0; k < nit; k += 4) {
+      step(k, xa, xb, q0, e0, q3, e3);
+      step(k + 1, xb, xa, q1, e1, q0, e0);
+      step(k + 2, xa, xb, q2, e2, q1, e1);
+      step(k + 3, xb, xa, q3, e3, q2, e2);
+    }
+    return;
+  }
+
+  // --------------------------------------------------------------- consumers
+  const int rg = wave;
+  float acc = 0.0f;
+  float4 win[C3_WIN];
+  auto src = [&](int c) { return &P[c % C3_RING][(rg * 64 + lane) * C3_LD]; };
+  __builtin_amdgcn_s_setprio(3);
+  for (int k = 0; k < nit; ++k) {
+    const int c = k - 2;
+    if (c == -1 && nch > 0) {
+      const float *p0 = src(0);
+#pragma unroll
+      for (int j = 0; j < C3_WIN; ++j) win[j] = *(const float4 *)(p0 + 4 * j);
+    } else if (c >= 0 && c < nch) {
+      const float *pc = src(c), *pn = src(c + 1);
+#pragma unroll
+      for (int j = 0; j < C3_CP / 4; ++j) {
+        const float4 v = win[j % C3_WIN];
+        if (!(DBG & 1)) {
+          acc = acc + v.x;
+          acc = acc + v.y;
+          acc = acc + v.z;
+          acc = acc + v.w;
+        }
+        const int jn = j + C3_WIN;
+        win[j % C3_WIN] = jn < C3_CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - C3_CP / 4));
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read x1
+      }
+    }
+    __syncthreads();
+  }
+
+  // ----------------------------------------------------------------- epilogue
+  const int row = (4 * g + 2 * rg) * T32 + lane;
+  const int rows = B.j[ji].w.rows;
+  const float *bias = B.j[ji].bias;
+  float *y = B.j[ji].y;
+  if (B.j[ji].epi == EPI_GELU_Q) {
+    const bool ok = row < rows;
+    float gv = 0.0f;
+    if (ok) {
+      gv = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      if (y) y[row] = gv;
+    }
+    const int blk = row / QK;
+    quantize_half(gv, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
+                  B.j[ji].oxd + (size_t)blk * QK);
+  } else if (row < rows) {
+    y[row] = bias ? acc + bias[row] : acc;
+  }
+}
+
 template <int DBG>
 static void chain_launch_t(int grid, const GemvBatch &B, hipStream_t s) {
   // (CB = 4 at two workgroups per CU measured slower than CB = 8 at one: the producers'
@@ -486,10 +646,16 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     const char *e = getenv("VSIM_CHAIN_ROWS");
     return e ? atoi(e) : 0;
   }();
-  int tiles = 0;
-  for (int i = 0; i < B.nj; ++i) tiles += B.j[i].w.tiles;
-  // 32-row workgroups when the 64-row grid would leave most CUs without a chain
-  const bool narrow = variant == 32 || (variant != 64 && groups < 192);
+  int tiles = 0, g128 = 0;
+  for (int i = 0; i < B.nj; ++i) {
+    tiles += B.j[i].w.tiles;
+    g128 += (B.j[i].w.tiles + 3) / 4;
+  }
+  // The widest variant whose grid still covers most of the 256 CUs: 128-row workgroups
+  // (two chains per CU) for large batches, 64-row, else 32-row (more CUs per row).
+  // VSIM_CHAIN_ROWS=32|64|128 forces one.
+  const int rows_per_wg = variant ? variant : g128 >= 192 ? 128 : groups >= 192 ? 64 : 32;
+  const bool narrow = rows_per_wg == 32;
   static const int dbg = [] {
     const char *e = getenv("VSIM_CHAIN_DBG");
     return e ? atoi(e) : 0;
@@ -503,6 +669,15 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
       case 6: hipLaunchKernelGGL(k_gemv_chain32<6>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
       case 7: hipLaunchKernelGGL(k_gemv_chain32<7>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
       default: hipLaunchKernelGGL(k_gemv_chain32<0>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;
+    }
+    VSIM_HIP(hipGetLastError());
+    return VSIM_OK;
+  }
+  if (rows_per_wg == 128) {
+    switch (dbg) {
+      case 1: hipLaunchKernelGGL(k_gemv_chain2<1>, dim3(g128), dim3(C3_THREADS), 0, s, B); break;
+      case 2: hipLaunchKernelGGL(k_gemv_chain2<2>, dim3(g128), dim3(C3_THREADS), 0, s, B); break;
+      default: hipLaunchKernelGGL(k_gemv_chain2<0>, dim3(g128), dim3(C3_THREADS), 0, s, B); break;
     }
     VSIM_HIP(hipGetLastError());
     return VSIM_OK;

@@ -79,6 +79,10 @@ struct vsim_model {
   int *npast_dev = nullptr, *npast_host = nullptr;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
+  // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
+  // fc_out, whose K = 4E chain is the layer's critical path
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int graph_mode = -1;
   int graph_kernels = 0;
 
@@ -363,7 +367,7 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
 }
 
 // GEMV profiling brackets (eager launches only; bench.py's live roofline)
-hipEvent_t *prof_begin(vsim_model *m) {
+hipEvent_t *prof_begin(vsim_model *m, hipStream_t st = nullptr) {
   if (!m->profile) return nullptr;
   if (m->prof_used + 2 > m->prof_events.size()) {
     hipEvent_t a, b;
@@ -373,12 +377,12 @@ hipEvent_t *prof_begin(vsim_model *m) {
   }
   hipEvent_t *ev = &m->prof_events[m->prof_used];
   m->prof_used += 2;
-  (void)hipEventRecord(ev[0], m->stream);
+  (void)hipEventRecord(ev[0], st ? st : m->stream);
   return ev;
 }
-void prof_end(vsim_model *m, hipEvent_t *ev, double bytes) {
+void prof_end(vsim_model *m, hipEvent_t *ev, double bytes, hipStream_t st = nullptr) {
   if (!ev) return;
-  (void)hipEventRecord(ev[1], m->stream);
+  (void)hipEventRecord(ev[1], st ? st : m->stream);
   m->prof_bytes += bytes;
 }
 
@@ -390,6 +394,13 @@ int enqueue_decode(vsim_model *m, int &nk) {
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
   const bool gptj = m->arch == VSIM_ARCH_GPTJ;
   hipStream_t s = m->stream;
+  // VSIM_SPLIT=1: the attention branch on a second stream beside fc_out.  Measured slower
+  // (413 vs 442 tok/s, GPT-J): each cross-queue event wait costs 4-10 us, more than the
+  // overlap wins.  Kept for A/B timing.
+  static const bool split = [] {
+    const char *e = getenv("VSIM_SPLIT");
+    return e && e[0] == '1';
+  }();
   DevTables tab;
   RC(tables_get(&tab));
   const int nbE = E / QK, nbF = F / QK;
@@ -429,9 +440,11 @@ int enqueue_decode(vsim_model *m, int &nk) {
     RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
     ++nk;
     if (pending) cur ^= 1;
-    // 2. {fc_in (+bias, GELU, requantize), Q, K, V (+bias)}
-    GemvBatch B{};
-    B.nj = 4;
+    // 2. fc_in (+bias, GELU, requantize) -> 3. fc_out; beside it, on the second stream,
+    //    Q/K/V -> attention -> out-projection.  fc_out's K = 4E chain (vsim.cpp:680-690) is
+    //    the longest dependency of the layer, so fc_in runs alone first (all CUs) and the
+    //    attention branch fills the CUs fc_out leaves idle.  Without split streams the same
+    //    work goes as two batches {fc_in, Q, K, V}, attention, {fc_out, out-proj}.
     auto job = [&](GemvBatch &Bt, int i, void *W, int M, int K, const float *xd, const uint8_t *xq, const float *xdd,
                    const float *bias, float *y) {
       GemvJob &J = Bt.j[i];
@@ -443,20 +456,36 @@ int enqueue_decode(vsim_model *m, int &nk) {
       J.y = y;
       J.epi = EPI_STORE;
     };
+    GemvBatch B{};
+    B.nj = split ? 1 : 4;
     job(B, 0, L.wfc, F, E, gptj ? m->xd1 : m->xd2, gptj ? q1 : q2, gptj ? d1 : d2, L.bfc, nullptr);
     B.j[0].epi = EPI_GELU_Q;
     B.j[0].gelu_tab = tab.gelu_f16;
     B.j[0].oq_qs = q3;
     B.j[0].oq_d = d3;
     B.j[0].oxd = m->xd3;
-    job(B, 1, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
-    job(B, 2, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
-    job(B, 3, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
+    GemvBatch Bq{};
+    GemvBatch &BQ = split ? Bq : B;
+    const int q0 = split ? 0 : 1;
+    BQ.nj = split ? 3 : 4;
+    job(BQ, q0 + 0, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
+    job(BQ, q0 + 1, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
+    job(BQ, q0 + 2, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
     hipEvent_t *ev = prof_begin(m);
     RC(launch_gemv_epi(B, m->mode, s));
-    prof_end(m, ev, w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
+    prof_end(m, ev, split ? w4_algo_bytes(B.j[0].w) : w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
     ++nk;
-    // 3. attention for the new token
+    hipStream_t sa = s;  // attention branch
+    if (split) {
+      sa = m->stream2;
+      VSIM_HIP(hipEventRecord(m->ev_fork, s));
+      VSIM_HIP(hipStreamWaitEvent(sa, m->ev_fork, 0));
+      ev = prof_begin(m, sa);
+      RC(launch_gemv_epi(BQ, m->mode, sa));
+      prof_end(m, ev, 3 * w4_algo_bytes(BQ.j[0].w), sa);
+      ++nk;
+    }
+    // attention for the new token
     AttnJob A{};
     A.q = m->Qb;
     A.k = m->Kb;
@@ -475,18 +504,28 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.oq_d = da;
     A.oxd = m->xda;
     A.out = nullptr;
-    RC(launch_attn_decode(A, m->n_ctx, s));
+    RC(launch_attn_decode(A, m->n_ctx, sa));
     ++nk;
-    // 4. {fc_out, out-projection} without biases (they join in the next norm); fc_out first
-    //    so its longer chains start first
+    // {fc_out, out-projection} without biases (they join in the next norm)
     GemvBatch B2{};
-    B2.nj = 2;
+    B2.nj = split ? 1 : 2;
     job(B2, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
-    job(B2, 1, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
+    GemvBatch Bo{};
+    GemvBatch &BO = split ? Bo : B2;
+    BO.nj = split ? 1 : 2;
+    job(BO, split ? 0 : 1, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
+    if (split) {
+      ev = prof_begin(m, sa);
+      RC(launch_gemv_epi(BO, m->mode, sa));
+      prof_end(m, ev, w4_algo_bytes(BO.j[0].w), sa);
+      ++nk;
+      VSIM_HIP(hipEventRecord(m->ev_join, sa));
+    }
     ev = prof_begin(m);
     RC(launch_gemv_epi(B2, m->mode, s));
-    prof_end(m, ev, w4_algo_bytes(B2.j[0].w) + w4_algo_bytes(B2.j[1].w));
+    prof_end(m, ev, split ? w4_algo_bytes(B2.j[0].w) : w4_algo_bytes(B2.j[0].w) + w4_algo_bytes(B2.j[1].w));
     ++nk;
+    if (split) VSIM_HIP(hipStreamWaitEvent(s, m->ev_join, 0));
     pending = true;
     pend_ab = gptj ? nullptr : L.bo;
     pend_fb = L.bproj;
@@ -575,7 +614,11 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   m->first = layer_begin == 0;
   m->last = layer_end == hp->n_layer;
   auto fail = [&](int rc) { vsim_model_free(m); return rc; };
-  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) return fail(hip_fail(hipErrorUnknown, "stream"));
+  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming) != hipSuccess)
+    return fail(hip_fail(hipErrorUnknown, "stream"));
   std::vector<std::pair<std::string, Slot>> plan;
   plan_slots(m, plan);
   size_t tot = 0;
@@ -620,6 +663,9 @@ void vsim_model_free(vsim_model *m) {
   if (m->vcache) (void)hipFree(m->vcache);
   if (m->rope_cs) (void)hipFree(m->rope_cs);
   if (m->stream) (void)hipStreamDestroy(m->stream);
+  if (m->stream2) (void)hipStreamDestroy(m->stream2);
+  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
   delete m;
 }
 
