@@ -50,6 +50,11 @@ def main():
         if not args.no_check:
             same = torch.equal(y.view(torch.int32), y2[:M].view(torch.int32))
             print(f"{name:16s} exact decode kernel bit-identical to row kernel: {same}", flush=True)
+            if not same:
+                bad = (y.view(torch.int32) != y2[:M].view(torch.int32)).nonzero().flatten().cpu()
+                rel = ((y - y2[:M]).abs() / y2[:M].abs().clamp_min(1e-30)).max().item()
+                print(f"    {bad.numel()} rows differ (first {bad[:8].tolist()}, row%32 set "
+                      f"{sorted(set((bad % 32).tolist()))[:12]}), max rel {rel:.3g}", flush=True)
         for mode in modes:
             for _ in range(3):
                 hip.check(L.vsim_op_q4_gemv(w.data_ptr(), M, K, xq.data_ptr(), xd.data_ptr(), 1, None, y.data_ptr(),

@@ -151,8 +151,14 @@ template <int NT>
 __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
                                const float *__restrict__ gb, unsigned *stats, const float *__restrict__ ja = nullptr,
                                const float *__restrict__ jab = nullptr, const float *__restrict__ jf = nullptr,
-                               const float *__restrict__ jfb = nullptr, float *__restrict__ jout = nullptr) {
+                               const float *__restrict__ jfb = nullptr, float *__restrict__ jout = nullptr,
+                               unsigned long long *prof = nullptr) {
   constexpr int NW = NT / 64;
+  // timing experiment (prof != null): phase stamps of thread 0
+  auto stamp = [&](int i) {
+    if (prof && threadIdx.x == 0) prof[i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   __shared__ double shs[NW], shsa[NW];
   __shared__ int shu[NW];
   __shared__ double bcast_d;
@@ -190,6 +196,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
       um = min(um, ulp_exp(e[j]));
     }
   }
+  stamp(1);
   s = wave_sum_d(s);
   sa = wave_sum_d(sa);
   um = wave_min_i(um);
@@ -227,6 +234,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     s = bcast_d;
   }
   const double mean = s / n;
+  stamp(2);
   double s2 = 0.0;
   for (int i = threadIdx.x; i < n4; i += NT) {
     const float4 v4 = ((const float4 *)row)[i];
@@ -244,6 +252,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   s2 = 0.0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) s2 += shs[w];
+  stamp(3);
   const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
   const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
   const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
@@ -261,6 +270,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     __syncthreads();
     scale = bcast_f;
   }
+  stamp(4);
   for (int i = threadIdx.x; i < n4; i += NT) {
     const float4 v4 = ((const float4 *)row)[i];
     float e[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -280,6 +290,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     ((float4 *)row)[i] = make_float4(e[0], e[1], e[2], e[3]);
   }
   __syncthreads();
+  stamp(5);
 }
 
 __device__ __forceinline__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
@@ -291,21 +302,26 @@ __device__ __forceinline__ void ln_exact_lds(const float *__restrict__ x, float 
 // quantize_row_q4_0 semantics (see quantize_block_lanes below).
 __device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
                                               float *xd_out) {
+  // amax over the half-wave: DPP within rows of 16 lanes, then rows 0<->1 and 2<->3 by
+  // ds_swizzle (xor 16); no LDS round trips in the dependent chain
+  auto mx = [](float a, float b) { return a > b ? a : b; };
   float a = fabsf(v);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    const float t = __shfl_xor(a, o, 64);
-    a = a > t ? a : t;
-  }
+  a = mx(a, dpp::mov<dpp::QP_XOR1, 0xF>(a, 0.0f));
+  a = mx(a, dpp::mov<dpp::QP_XOR2, 0xF>(a, 0.0f));
+  a = mx(a, dpp::mov<dpp::HALF_MIRROR, 0xF>(a, 0.0f));
+  a = mx(a, dpp::mov<dpp::MIRROR, 0xF>(a, 0.0f));
+  a = mx(a, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(a), 0x401F)));
   const float d = a / 7.0f;
   const float id = d != 0.0f ? 1.0f / d : 0.0f;
   const int q = x86_round_i8(v * id) + 8;
   const int l = lane & 31;
-  const int qn = __shfl_xor(q, 1, 64);
-  const uint32_t byte = (l & 1) ? 0u : (uint32_t)((q & 0xF) | ((qn & 0xF) << 4));
+  // byte of pair l/2 (nibbles of lanes 2j, 2j+1), then OR of each 8-lane group's bytes into
+  // its word: xor 1, xor 2, and the half-row mirror (lane i <-> 7-i) reach all 8 lanes
+  const int qn = dpp::mov<dpp::QP_XOR1, 0xF>(q, 0);
+  const uint32_t byte = (l & 1) ? (uint32_t)((qn & 0xF) | ((q & 0xF) << 4)) : (uint32_t)((q & 0xF) | ((qn & 0xF) << 4));
   uint32_t word = byte << (8 * ((l >> 1) & 3));
-  word |= __shfl_xor(word, 2, 64);
-  word |= __shfl_xor(word, 4, 64);
+  word |= (uint32_t)dpp::mov<dpp::QP_XOR2, 0xF>((int)word, 0);
+  word |= (uint32_t)dpp::mov<dpp::HALF_MIRROR, 0xF>((int)word, 0);
   if (ok) {
     if ((l & 7) == 0) ((uint32_t *)qs_out)[l >> 3] = word;
     if (l == 0) *d_out = d;

@@ -27,10 +27,14 @@ extern unsigned *g_norm_stats;
 // One 1024-thread workgroup per LayerNorm (two for GPT-NeoX's parallel-residual pair); the
 // normalized row is quantized by whole waves, two 32-blocks per wave step.
 constexpr int LNQ_THREADS = 1024;
+__device__ unsigned long long g_ln_prof[8];  // timing experiment output (VSIM_LN_DBG)
+
+template <bool PROF>
 __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float row[];
   const LnQuantJob &J = blockIdx.x == 0 ? j0 : j1;
-  ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, stats, J.ja, J.jab, J.jf, J.jfb, J.jout);
+  unsigned long long *prof = PROF && blockIdx.x == 0 ? g_ln_prof : nullptr;
+  ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, stats, J.ja, J.jab, J.jf, J.jfb, J.jout, prof);
   const int nb = n / QK, lane = threadIdx.x & 63;
   for (int b2 = threadIdx.x >> 6; 2 * b2 < nb; b2 += LNQ_THREADS / 64) {
     const int b = 2 * b2 + (lane >> 5);
@@ -38,11 +42,17 @@ __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuant
     const float v = ok ? row[b * QK + (lane & 31)] : 0.0f;
     quantize_half(v, lane, ok, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
   }
+  if (PROF && blockIdx.x == 0 && threadIdx.x == 0) g_ln_prof[6] = __builtin_amdgcn_s_memtime();
 }
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_ln_quant, dim3(j1 ? 2 : 1), dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
-                     g_norm_stats);
+  static const bool prof = getenv("VSIM_LN_DBG") != nullptr;
+  if (prof)
+    hipLaunchKernelGGL(k_ln_quant<true>, dim3(j1 ? 2 : 1), dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0,
+                       n, g_norm_stats);
+  else
+    hipLaunchKernelGGL(k_ln_quant<false>, dim3(j1 ? 2 : 1), dim3(LNQ_THREADS), (size_t)n * 4, s, j0,
+                       j1 ? *j1 : j0, n, g_norm_stats);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -278,3 +288,7 @@ int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s) {
 }
 
 }  // namespace vsim
+
+extern "C" int vsim_debug_ln_prof(unsigned long long *out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(vsim::g_ln_prof), sizeof(vsim::g_ln_prof)) == hipSuccess ? 0 : -1;
+}
