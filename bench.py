@@ -274,11 +274,13 @@ def main():
     tok = int(np.argmax(logits))
 
     def run_steps(k):
+        # greedy decode kept on the device (vsim_model_generate): each step's argmax feeds
+        # the next without a host round trip; the same tokens as eval() + numpy.argmax
+        # (tests/test_gpu_model.py::test_generate_matches_stepwise_greedy)
         nonlocal n_past, tok
-        for _ in range(k):
-            lg = model.eval(n_past, [tok])
-            n_past += 1
-            tok = int(np.argmax(lg))
+        if k:
+            tok = model.generate(n_past, tok, k)[-1]
+            n_past += k
 
     run_steps(args.warmup)
 

@@ -139,6 +139,16 @@ int vsim_model_hparams(const vsim_model *m, vsim_hparams *hp, int *n_ctx, int *l
  * the last row of logits to `logits` (host, n_vocab floats) if non-NULL. */
 int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, const float *resid_in,
                     float *resid_out, float *logits);
+/* Greedy single-token decode step of a whole-model stage: eval of `token` at n_past, then
+ * the argmax of the logits on the device (numpy.argmax conventions: first maximum, first
+ * NaN); only the token id leaves the device.  The reference's loop samples on the host
+ * from the logits (vsim.cpp:860-891); this is its greedy case without the logits copy. */
+int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *next_token);
+/* Device-resident greedy generation: n_steps single-token steps from (n_past, token), each
+ * step's argmax feeding the next on the device (no host round trip per token); the
+ * n_steps generated tokens are copied to tokens_out at the end.  Same tokens as calling
+ * vsim_model_eval_argmax n_steps times. */
+int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, int32_t *tokens_out);
 /* Decode-step timing helpers for bench.py: the stream the executor launches on, and
  * device pointers of the last logits / residual buffers. */
 void *vsim_model_stream(vsim_model *m);

@@ -156,3 +156,46 @@ def test_graph_replay_bit_exact_vs_oracle(cfg, tmp_path):
         assert np.array_equal(lo.view(np.uint32), ld.view(np.uint32)), step
         n_past += 1
     assert dm.info()["graph"]
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_eval_argmax_matches_logits(graph, tmp_path):
+    """The greedy step (device argmax, vsim_model_eval_argmax) returns numpy.argmax of the
+    logits of the same eval: re-evaluating a position rewrites the same cache row, so
+    both calls see the same state."""
+    arch_s, hp = mg.CONFIGS["small-gptj"]
+    path = str(tmp_path / "g.bin")
+    mg.write_model(path, arch_s, hp, seed=5, std=0.05)
+    m = hip.Model.load(path, hip.ARCH_GPTJ)
+    m.set_graph(graph)
+    lg = m.eval(0, [3, 1, 4, 1, 5])
+    n_past, tok = 5, int(np.argmax(lg))
+    for _ in range(12):
+        lg = m.eval(n_past, [tok])
+        nxt = m.eval_argmax(n_past, tok)
+        assert nxt == int(np.argmax(lg))
+        n_past, tok = n_past + 1, nxt
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_generate_matches_stepwise_greedy(graph, tmp_path):
+    """The device-resident greedy loop (vsim_model_generate) produces the tokens of the
+    host-driven loop eval() + numpy.argmax."""
+    arch_s, hp = mg.CONFIGS["small-gptj"]
+    path = str(tmp_path / "gen.bin")
+    mg.write_model(path, arch_s, hp, seed=6, std=0.05)
+    a = hip.Model.load(path, hip.ARCH_GPTJ)
+    b = hip.Model.load(path, hip.ARCH_GPTJ)
+    a.set_graph(graph)
+    b.set_graph(graph)
+    prompt = [2, 7, 1, 8]
+    tok = int(np.argmax(a.eval(0, prompt)))
+    assert tok == int(np.argmax(b.eval(0, prompt)))
+    ref, n_past, t = [], len(prompt), tok
+    for _ in range(16):
+        t = int(np.argmax(a.eval(n_past, [t])))
+        ref.append(t)
+        n_past += 1
+    got = b.generate(len(prompt), tok, 10)  # in two calls: the loop resumes from (n_past, token)
+    got += b.generate(len(prompt) + 10, got[-1], 6)
+    assert got == ref

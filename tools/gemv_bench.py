@@ -77,6 +77,13 @@ def main():
                 buf = (ctypes.c_ulonglong * 64)()
                 L.vsim_debug_chain_prof(buf)
                 nit = max(buf[4], 1)
+                if os.environ.get("VSIM_SOLO"):
+                    print(f"    consumer per iter (ticks): adds {buf[8] / nit:.0f} barrier {buf[9] / nit:.0f}  (iters {nit})")
+                    for w in range(int(os.environ["VSIM_SOLO"])):
+                        b = buf[16 + 4 * w: 19 + 4 * w]
+                        print(f"      producer {w}: top+wait {b[0] / nit:5.0f} compute {b[1] / nit:5.0f} "
+                              f"barrier {b[2] / nit:5.0f}", flush=True)
+                    continue
                 print(f"    producer per iter (cycles): lds-wait {buf[0] / nit:.0f} compute {buf[1] / nit:.0f} "
                       f"dma+vmwait {buf[2] / nit:.0f} barrier {buf[3] / nit:.0f} | consumer: adds {buf[8] / nit:.0f} "
                       f"barrier {buf[9] / nit:.0f}  (iters {nit})", flush=True)

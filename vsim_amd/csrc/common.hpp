@@ -229,6 +229,8 @@ int launch_act_unpack(const void *xq, void *aos, int n, int k, hipStream_t s);
 int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s);
 int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s);
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
+int launch_argmax(const float *x, int n, int *out, hipStream_t s);
+int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
 int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s);
 int launch_rope(int style, float *x, int d, int H, int T, int n_past, int n_dims, int mode,

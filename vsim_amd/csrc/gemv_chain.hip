@@ -47,6 +47,14 @@ typedef const __attribute__((address_space(4))) float sfloat;  // scalar-loaded
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
 
+// Producer-side barrier without the lgkmcnt(0) of __syncthreads: it would also wait for the
+// scalar loads of the next chunk's activation factors still in flight.  The pair terms
+// written before it are first read by the consumer one whole chunk later (it reads chunk
+// k-1 near the end of iteration k), and the slot reuse is guarded by the consumer's own
+// full wait before its barrier.  The "memory" clobber keeps the compiler from moving the
+// stores across.
+__device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
 // LDS-DMA: each lane's 16 (4) bytes from its own global address land lane-linearly at the
 // wave-uniform LDS address.  Inline asm keeps the load out of the compiler's wait-count
 // bookkeeping: completion is retired by the explicit vmcnt waits.  nt: streamed once.
@@ -623,6 +631,204 @@ __global__ void __launch_bounds__(C3_THREADS, 1) k_gemv_chain2(GemvBatch B) {
   }
 }
 
+// ================================================================== 64-row, SIMD0 solo
+// For jobs whose chains are the whole cost (fc_out: K = 16384 over only 4096 rows): the
+// consumer wave alone on SIMD0 (producers sharing its SIMD stretch each dependent add by a
+// VALU slot), CB producer waves on SIMD1-3, one Q4_0 block of the chunk for the 64 rows
+// each, so the activation factors are wave-uniform scalar loads and the LDS carries
+// nothing but pair terms.  Waves the hardware would place on SIMD0 (4, 8, ...) only join
+// the barriers.  Weights: register ring as k_gemv_chain2.
+template <int CB>
+struct SoloShape {
+  static constexpr int CP = CB * 16, LD = CP + 4;
+  static constexpr int WAVES = 1 + CB + (CB - 1) / 3;  // consumer, producers, SIMD0 fillers
+  static constexpr int WIN = CP / 4 % 8 == 0 ? 8 : 12;
+  static_assert(CP / 4 % WIN == 0, "the read window must tile the chunk");
+  static_assert(WAVES <= 16, "workgroup size");
+};
+constexpr int C5_RING = 3;
+
+// PF: prefetch distance of the weight loads in chunks (register ring of PF+1 sets)
+template <int DBG, int CB, int PF>
+__global__ void __launch_bounds__(64 * SoloShape<CB>::WAVES, 1) k_gemv_solo(GemvBatch B) {
+  using S = SoloShape<CB>;
+  __shared__ __attribute__((aligned(16))) float P[C5_RING][64 * S::LD];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  int g = blockIdx.x, ji = 0;
+  while (ji < B.nj) {
+    const int ng = (B.j[ji].w.tiles + 1) / 2;
+    if (g < ng) break;
+    g -= ng;
+    ++ji;
+  }
+  if (ji >= B.nj) return;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  g = __builtin_amdgcn_readfirstlane(g);
+  const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
+  const int nit = (nch + 2 + PF) / (PF + 1) * (PF + 1);
+
+  if (wave != 0 && (wave & 3) == 0) {  // SIMD0 filler
+    for (int k = 0; k < nit; ++k) __syncthreads();
+    return;
+  }
+  if (wave > 0) {
+    // ------------------------------------------------------------- producer
+    const int o = wave - 1 - (wave >> 2);  // 1,2,3,5,6,7,9,... -> 0,1,2,...
+    const int h = lane >> 5, r = lane & 31;
+    const int tile = 2 * g + h;
+    const bool tile_ok = tile < tiles;
+    const int tl = tile_ok ? tile : tiles - 1;
+    const uint8_t *qs = B.j[ji].w.qs + ((size_t)tl * nb * T32 + r) * 16;
+    const float *dd = B.j[ji].w.d + (size_t)tl * nb * T32 + r;
+    const float *xg = B.j[ji].xd;
+    auto ld = [&](int c, u32x4 &qv, float &dv) {
+      const int b = min(c * CB + o, nb - 1);
+      qv = __builtin_nontemporal_load((gu32x4 *)(qs + (size_t)b * (T32 * 16)));
+      dv = __builtin_nontemporal_load((gfloat *)(dd + (size_t)b * T32));
+    };
+    auto ldx = [&](int c, f32x2 *xv) {
+      const int b = min(c * CB + o, nb - 1);
+      const sfloat *xp = (const sfloat *)(xg + (size_t)b * QK);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        xv[i].x = xp[2 * i];
+        xv[i].y = xp[2 * i + 1];
+      }
+    };
+    int ps = 0;
+    unsigned long long pt[4] = {0, 0, 0, 0}, tp = 0;
+    auto stamp = [&](int i) {
+      if (DBG & 8) {
+        const unsigned long long tt = __builtin_amdgcn_s_memtime();
+        if (i >= 0) pt[i] += tt - tp;
+        tp = tt;
+      }
+    };
+    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
+      stamp(-1);
+      ld(k + PF, qn, dqn);
+      // this chunk's factors (loaded a whole step ago) before the next chunk's loads go out:
+      // scalar loads return out of order, so any later wait for them would be lgkmcnt(0)
+      // and would also wait for the loads just issued
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+      stamp(0);
+      ldx(k + 1, xn);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(DBG & 2)) {
+        const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
+        const float dl = 512.0f * dv, ml = -8.0f * dv;
+        float dh, mh;
+        asm("v_mov_b32 %0, %1" : "=v"(dh) : "v"(dl));  // see k_gemv_chain2
+        asm("v_mov_b32 %0, %1" : "=v"(mh) : "v"(ml));
+        const f32x2 d2 = {dl, dh}, m2 = {ml, mh};
+        float *dst = &P[ps][lane * S::LD + o * 16];
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) {
+          float p4[4];
+          pair_terms4_x(qc[wv], d2, m2, xc + 4 * wv, p4);
+          *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+        }
+      }
+      ps = ps == C5_RING - 1 ? 0 : ps + 1;
+      __builtin_amdgcn_sched_barrier(0);
+      stamp(1);
+      if (DBG & 4)
+        __syncthreads();
+      else
+        producer_barrier();
+      stamp(2);
+    };
+    u32x4 q[PF + 1];
+    float e[PF + 1];
+#pragma unroll
+    for (int c = 0; c < PF; ++c) ld(c, q[c], e[c]);
+    f32x2 xa[16], xb[16];
+    ldx(0, xa);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("" ::"s"(xa[i].x), "s"(xa[i].y));
+    static_assert((PF + 1) % 2 == 0, "two factor sets alternate");
+    for (int k = 0; k < nit; k += PF + 1) {
+#pragma unroll
+      for (int u = 0; u < PF + 1; u += 2) {
+        step(k + u, xa, xb, q[u], e[u], q[(u + PF) % (PF + 1)], e[(u + PF) % (PF + 1)]);
+        step(k + u + 1, xb, xa, q[u + 1], e[u + 1], q[u % (PF + 1)], e[u % (PF + 1)]);
+      }
+    }
+    if ((DBG & 8) && blockIdx.x == 0 && lane == 0) {
+      for (int i = 0; i < 3; ++i) g_chain_prof[16 + 4 * o + i] = pt[i];
+      if (o == 0) g_chain_prof[4] = nit;
+    }
+    return;
+  }
+
+  // --------------------------------------------------------------- consumer
+  float acc = 0.0f;
+  float4 win[S::WIN];
+  auto src = [&](int c) { return &P[c % C5_RING][lane * S::LD]; };
+  __builtin_amdgcn_s_setprio(3);
+  unsigned long long ct[2] = {0, 0}, tc = 0;
+  auto cstamp = [&](int i) {
+    if (DBG & 8) {
+      const unsigned long long tt = __builtin_amdgcn_s_memtime();
+      if (i >= 0) ct[i] += tt - tc;
+      tc = tt;
+    }
+  };
+  for (int k = 0; k < nit; ++k) {
+    cstamp(-1);
+    const int c = k - 2;
+    if (c == -1 && nch > 0) {
+      const float *p0 = src(0);
+#pragma unroll
+      for (int j = 0; j < S::WIN; ++j) win[j] = *(const float4 *)(p0 + 4 * j);
+    } else if (c >= 0 && c < nch) {
+      const float *pc = src(c), *pn = src(c + 1);
+#pragma unroll
+      for (int j = 0; j < S::CP / 4; ++j) {
+        const float4 v = win[j % S::WIN];
+        if (!(DBG & 1)) {
+          acc = acc + v.x;
+          acc = acc + v.y;
+          acc = acc + v.z;
+          acc = acc + v.w;
+        }
+        const int jn = j + S::WIN;
+        win[j % S::WIN] = jn < S::CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - S::CP / 4));
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read x1
+      }
+    }
+    cstamp(0);
+    __syncthreads();
+    cstamp(1);
+  }
+  if ((DBG & 8) && blockIdx.x == 0 && lane == 0) {
+    g_chain_prof[8] = ct[0];
+    g_chain_prof[9] = ct[1];
+  }
+
+  // ----------------------------------------------------------------- epilogue
+  const int row = g * 64 + lane;
+  const int rows = B.j[ji].w.rows;
+  const float *bias = B.j[ji].bias;
+  float *y = B.j[ji].y;
+  if (B.j[ji].epi == EPI_GELU_Q) {
+    const bool ok = row < rows;
+    float gv = 0.0f;
+    if (ok) {
+      gv = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      if (y) y[row] = gv;
+    }
+    const int blk = row / QK;
+    quantize_half(gv, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
+                  B.j[ji].oxd + (size_t)blk * QK);
+  } else if (row < rows) {
+    y[row] = bias ? acc + bias[row] : acc;
+  }
+}
+
 template <int DBG>
 static void chain_launch_t(int grid, const GemvBatch &B, hipStream_t s) {
   // (CB = 4 at two workgroups per CU measured slower than CB = 8 at one: the producers'
@@ -654,12 +860,41 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
   // The widest variant whose grid still covers most of the 256 CUs: 128-row workgroups
   // (two chains per CU) for large batches, 64-row, else 32-row (more CUs per row).
   // VSIM_CHAIN_ROWS=32|64|128 forces one.
-  const int rows_per_wg = variant ? variant : g128 >= 192 ? 128 : groups >= 192 ? 64 : 32;
+  // default: 64-row SIMD0-solo workgroups when there are enough of them to cover the CUs,
+  // else 32-row ones (more CUs per row: fc_out and the out-projection)
+  const int rows_per_wg = variant ? variant : groups >= 192 ? 640 : 32;
   const bool narrow = rows_per_wg == 32;
   static const int dbg = [] {
     const char *e = getenv("VSIM_CHAIN_DBG");
     return e ? atoi(e) : 0;
   }();
+  static const int solo_env = [] {  // VSIM_SOLO=6|9: the 64-row SIMD0-solo kernel for every batch
+    const char *e = getenv("VSIM_SOLO");
+    return e ? atoi(e) : 0;
+  }();
+  const int solo_cb = solo_env ? solo_env : rows_per_wg == 640 ? 6 : 0;
+  if (solo_cb) {
+    static const int pf = [] {
+      const char *e = getenv("VSIM_SOLO_PF");
+      return e ? atoi(e) : 3;
+    }();
+#define C5L(D, CB, PF) hipLaunchKernelGGL((k_gemv_solo<D, CB, PF>), dim3(groups), dim3(64 * SoloShape<CB>::WAVES), 0, s, B)
+    if (solo_cb == 9) {
+      if (pf == 7) C5L(0, 9, 7); else C5L(0, 9, 3);
+    } else {
+      if (pf == 7) {
+        if (dbg == 1) C5L(1, 6, 7); else if (dbg == 2) C5L(2, 6, 7); else C5L(0, 6, 7);
+      } else if (pf == 5) {
+        C5L(0, 6, 5);
+      } else {
+        if (dbg == 1) C5L(1, 6, 3); else if (dbg == 2) C5L(2, 6, 3); else if (dbg == 4) C5L(4, 6, 3);
+        else if (dbg == 8) C5L(8, 6, 3); else if (dbg == 9) C5L(9, 6, 3); else C5L(0, 6, 3);
+      }
+    }
+#undef C5L
+    VSIM_HIP(hipGetLastError());
+    return VSIM_OK;
+  }
   if (narrow) {
     switch (dbg) {
       case 1: hipLaunchKernelGGL(k_gemv_chain32<1>, dim3(tiles), dim3(C2_THREADS), 0, s, B); break;

@@ -79,6 +79,17 @@ struct vsim_model {
   int *npast_dev = nullptr, *npast_host = nullptr;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
+  // greedy variant of the decode graph: device argmax, 4-byte copy-out instead of the logits
+  hipGraph_t graph_am = nullptr;
+  hipGraphExec_t gexec_am = nullptr;
+  int graph_am_mode = -1;
+  int *am_dev = nullptr, *am_host = nullptr;
+  // device-resident greedy loop (vsim_model_generate): graph without uploads; the argmax
+  // kernel feeds tok_dev / npast_dev and records into hist_dev[n_ctx]
+  hipGraph_t graph_gen = nullptr;
+  hipGraphExec_t gexec_gen = nullptr;
+  int graph_gen_mode = -1;
+  int *hist_dev = nullptr;
   // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
   // fc_out, whose K = 4E chain is the layer's critical path
   hipStream_t stream2 = nullptr;
@@ -107,6 +118,21 @@ void free_scratch(vsim_model *m) {
   if (m->logit_host) (void)hipHostFree(m->logit_host);
   if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
   if (m->graph) (void)hipGraphDestroy(m->graph);
+  if (m->gexec_am) (void)hipGraphExecDestroy(m->gexec_am);
+  if (m->graph_am) (void)hipGraphDestroy(m->graph_am);
+  if (m->am_dev) (void)hipFree(m->am_dev);
+  if (m->am_host) (void)hipHostFree(m->am_host);
+  m->gexec_am = nullptr;
+  m->graph_am = nullptr;
+  m->graph_am_mode = -1;
+  m->am_dev = m->am_host = nullptr;
+  if (m->gexec_gen) (void)hipGraphExecDestroy(m->gexec_gen);
+  if (m->graph_gen) (void)hipGraphDestroy(m->graph_gen);
+  if (m->hist_dev) (void)hipFree(m->hist_dev);
+  m->gexec_gen = nullptr;
+  m->graph_gen = nullptr;
+  m->graph_gen_mode = -1;
+  m->hist_dev = nullptr;
   if (m->xqa) (void)hipFree(m->xqa);
   if (m->xda) (void)hipFree(m->xda);
   if (m->inpL2) (void)hipFree(m->inpL2);
@@ -163,6 +189,9 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(fa(&m->inpL2, E));
   VSIM_HIP(hipMalloc((void **)&m->npast_dev, sizeof(int)));
   VSIM_HIP(hipHostMalloc((void **)&m->npast_host, sizeof(int), hipHostMallocDefault));
+  VSIM_HIP(hipMalloc((void **)&m->am_dev, sizeof(int)));
+  VSIM_HIP(hipHostMalloc((void **)&m->am_host, sizeof(int), hipHostMallocDefault));
+  VSIM_HIP(hipMalloc((void **)&m->hist_dev, (size_t)m->n_ctx * sizeof(int)));
   m->n_max = n;
   return VSIM_OK;
 }
@@ -796,6 +825,144 @@ int vsim_model_info(vsim_model *m, int *kernels_per_eval, int *graph_enabled, si
   return VSIM_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// token (first stage) and n_past from their pinned host words
+int upload_step(vsim_model *m) {
+  if (m->first)
+    VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, sizeof(int32_t), hipMemcpyHostToDevice, m->stream));
+  VSIM_HIP(hipMemcpyAsync(m->npast_dev, m->npast_host, sizeof(int), hipMemcpyHostToDevice, m->stream));
+  return VSIM_OK;
+}
+
+// Capture (once per mode) the whole single-token step as a hipGraph: uploads, the decode
+// kernels, and either the logits copy-out or the device argmax and its 4-byte copy-out.
+// kind 2: the device-resident greedy loop's step -- no uploads, no copy-out; the argmax
+// feeds the next step (launch_argmax_gen).
+int decode_graph(vsim_model *m, int kind) {
+  const bool argmax = kind == 1, gen = kind == 2;
+  hipGraph_t &graph = gen ? m->graph_gen : argmax ? m->graph_am : m->graph;
+  hipGraphExec_t &gexec = gen ? m->gexec_gen : argmax ? m->gexec_am : m->gexec;
+  int &gmode = gen ? m->graph_gen_mode : argmax ? m->graph_am_mode : m->graph_mode;
+  if (gexec && gmode == m->mode) return VSIM_OK;
+  if (gexec) (void)hipGraphExecDestroy(gexec);
+  if (graph) (void)hipGraphDestroy(graph);
+  gexec = nullptr;
+  graph = nullptr;
+  hipStream_t s = m->stream;
+  const int V = m->hp.n_vocab;
+  VSIM_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  int gk = 0;
+  int rc = gen ? VSIM_OK : upload_step(m);
+  if (rc == 0) rc = enqueue_decode(m, gk);
+  if (rc == 0 && gen) {
+    rc = launch_argmax_gen(m->logits, V, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s);
+    ++gk;
+  } else if (rc == 0 && argmax) {
+    rc = launch_argmax(m->logits, V, m->am_dev, s);
+    ++gk;
+    if (rc == 0 && hipMemcpyAsync(m->am_host, m->am_dev, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
+      rc = hip_fail(hipErrorUnknown, "capture argmax copy");
+  } else if (rc == 0 &&
+             hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s) != hipSuccess) {
+    rc = hip_fail(hipErrorUnknown, "capture logits copy");
+  }
+  hipGraph_t g = nullptr;
+  const hipError_t ce = hipStreamEndCapture(s, &g);
+  if (rc) return rc;
+  if (ce != hipSuccess) return hip_fail(ce, "hipStreamEndCapture");
+  graph = g;
+  VSIM_HIP(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+  gmode = m->mode;
+  m->graph_kernels = gk;
+  return VSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *next_token) {
+  if (!m || !next_token) { set_error("eval_argmax: null argument"); return VSIM_EINVAL; }
+  if (!m->first || !m->last || !fused_ok(m, 1)) {
+    set_error("eval_argmax: needs a whole-model stage with the single-token decode path");
+    return VSIM_EINVAL;
+  }
+  if (n_past < 0 || n_past + 1 > m->n_ctx) { set_error("eval_argmax: n_past + 1 exceeds n_ctx"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, 1));
+  const int V = m->hp.n_vocab;
+  if (token < 0 || token >= V) { set_error("eval_argmax: token id out of range"); return VSIM_EINVAL; }
+  m->tok_host[0] = token;
+  m->npast_host[0] = n_past;
+  hipStream_t s = m->stream;
+  if (m->graph_enabled && !m->profile) {
+    RC(decode_graph(m, 1));
+    VSIM_HIP(hipGraphLaunch(m->gexec_am, s));
+    m->kernels_last = m->graph_kernels;
+  } else {
+    int nk = 0;
+    RC(upload_step(m));
+    RC(enqueue_decode(m, nk));
+    RC(launch_argmax(m->logits, V, m->am_dev, s));
+    VSIM_HIP(hipMemcpyAsync(m->am_host, m->am_dev, sizeof(int), hipMemcpyDeviceToHost, s));
+    m->kernels_last = nk + 1;
+  }
+  VSIM_HIP(hipStreamSynchronize(s));
+  *next_token = m->am_host[0];
+  if (m->profile) {
+    for (size_t i = 0; i + 1 < m->prof_used; i += 2) {
+      float ms = 0.0f;
+      VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[i], m->prof_events[i + 1]));
+      m->prof_ms += ms;
+      ++m->prof_launches;
+    }
+    m->prof_used = 0;
+  }
+  return VSIM_OK;
+}
+
+int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, int32_t *tokens_out) {
+  if (!m || !tokens_out || n_steps < 0) { set_error("generate: bad argument"); return VSIM_EINVAL; }
+  if (!m->first || !m->last || !fused_ok(m, 1)) {
+    set_error("generate: needs a whole-model stage with the single-token decode path");
+    return VSIM_EINVAL;
+  }
+  if (n_past < 0 || n_past + n_steps > m->n_ctx) { set_error("generate: n_past + n_steps exceeds n_ctx"); return VSIM_EINVAL; }
+  if (n_steps == 0) return VSIM_OK;
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, 1));
+  if (token < 0 || token >= m->hp.n_vocab) { set_error("generate: token id out of range"); return VSIM_EINVAL; }
+  hipStream_t s = m->stream;
+  m->tok_host[0] = token;
+  m->npast_host[0] = n_past;
+  RC(upload_step(m));
+  if (m->graph_enabled && !m->profile) {
+    RC(decode_graph(m, 2));
+    for (int i = 0; i < n_steps; ++i) VSIM_HIP(hipGraphLaunch(m->gexec_gen, s));
+  } else {
+    for (int i = 0; i < n_steps; ++i) {
+      int nk = 0;
+      RC(enqueue_decode(m, nk));
+      RC(launch_argmax_gen(m->logits, m->hp.n_vocab, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s));
+    }
+  }
+  VSIM_HIP(hipMemcpyAsync(tokens_out, m->hist_dev + n_past, sizeof(int32_t) * n_steps, hipMemcpyDeviceToHost, s));
+  VSIM_HIP(hipStreamSynchronize(s));
+  if (m->profile) {
+    for (size_t i = 0; i + 1 < m->prof_used; i += 2) {
+      float ms = 0.0f;
+      VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[i], m->prof_events[i + 1]));
+      m->prof_ms += ms;
+      ++m->prof_launches;
+    }
+    m->prof_used = 0;
+  }
+  return VSIM_OK;
+}
+
 int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, const float *resid_in, float *resid_out,
                     float *logits) {
   if (N <= 0 || n_past < 0 || n_past + N > m->n_ctx) { set_error("eval: n_past + N exceeds n_ctx"); return VSIM_EINVAL; }
@@ -809,38 +976,20 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
       if (!tokens) { set_error("eval: first stage needs tokens"); return VSIM_EINVAL; }
       if (tokens[0] < 0 || tokens[0] >= V) { set_error("eval: token id out of range"); return VSIM_EINVAL; }
       m->tok_host[0] = tokens[0];
-      VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, sizeof(int32_t), hipMemcpyHostToDevice, s));
     } else {
       if (!resid_in) { set_error("eval: non-first stage needs resid_in"); return VSIM_EINVAL; }
       VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
     }
     m->npast_host[0] = n_past;
-    VSIM_HIP(hipMemcpyAsync(m->npast_dev, m->npast_host, sizeof(int), hipMemcpyHostToDevice, s));
     const bool use_graph = m->graph_enabled && m->first && m->last && !m->profile;
     if (use_graph) {
-      if (!m->gexec || m->graph_mode != m->mode) {
-        if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
-        if (m->graph) (void)hipGraphDestroy(m->graph);
-        m->gexec = nullptr;
-        m->graph = nullptr;
-        VSIM_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        int gk = 0;
-        int rc = enqueue_decode(m, gk);
-        if (rc == 0 && hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s) !=
-                           hipSuccess)
-          rc = hip_fail(hipErrorUnknown, "capture logits copy");
-        hipGraph_t g = nullptr;
-        const hipError_t ce = hipStreamEndCapture(s, &g);
-        if (rc) return rc;
-        if (ce != hipSuccess) return hip_fail(ce, "hipStreamEndCapture");
-        m->graph = g;
-        VSIM_HIP(hipGraphInstantiate(&m->gexec, m->graph, nullptr, nullptr, 0));
-        m->graph_mode = m->mode;
-        m->graph_kernels = gk;
-      }
+      // the token / n_past uploads are nodes of the graph (they read the pinned host words
+      // when the graph runs)
+      RC(decode_graph(m, 0));
       VSIM_HIP(hipGraphLaunch(m->gexec, s));
       nk = m->graph_kernels;
     } else {
+      RC(upload_step(m));
       RC(enqueue_decode(m, nk));
       if (m->last && logits)
         VSIM_HIP(hipMemcpyAsync(m->logit_host, m->logits, sizeof(float) * V, hipMemcpyDeviceToHost, s));

@@ -195,4 +195,74 @@ int norm_stats(unsigned *out2) {
   return VSIM_OK;
 }
 
+// ------------------------------------------------------------------ greedy argmax
+// Index of the largest logit with numpy.argmax's conventions: the first index among equal
+// maxima, and the first NaN if there is one.  One 1024-thread workgroup.
+__device__ __forceinline__ bool am_better(float v, int i, float bv, int bi) {
+  const bool n = v != v, bn = bv != bv;
+  if (n != bn) return n;
+  if (n) return i < bi;
+  if (v != bv) return v > bv;
+  return i < bi;
+}
+// GEN: the device-resident greedy loop's epilogue -- the token also becomes the next step's
+// input (tok), is recorded at hist[n_past] and n_past advances (k_argmax is the last kernel
+// of the step, so every reader of n_past has run).
+template <bool GEN>
+__global__ void __launch_bounds__(1024) k_argmax(const float *__restrict__ x, int n, int *__restrict__ out,
+                                                 int *tok, int *npast, int *hist) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  float bv = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const float v = x[i];
+    if (am_better(v, i, bv, bi)) {
+      bv = v;
+      bi = i;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v = __shfl_xor(bv, o, 64);
+    const int i = __shfl_xor(bi, o, 64);
+    if (am_better(v, i, bv, bi)) {
+      bv = v;
+      bi = i;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sv[w] = bv;
+    si[w] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 16; ++k)
+      if (am_better(sv[k], si[k], bv, bi)) {
+        bv = sv[k];
+        bi = si[k];
+      }
+    *out = bi;
+    if (GEN) {
+      const int np = *npast;
+      *tok = bi;
+      hist[np] = bi;
+      *npast = np + 1;
+    }
+  }
+}
+
+int launch_argmax(const float *x, int n, int *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_argmax<false>, dim3(1), dim3(1024), 0, s, x, n, out, nullptr, nullptr, nullptr);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s) {
+  hipLaunchKernelGGL(k_argmax<true>, dim3(1), dim3(1024), 0, s, x, n, out, tok, npast, hist);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
 }  // namespace vsim

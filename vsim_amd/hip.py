@@ -31,7 +31,8 @@ EXPORTS = [
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
     "vsim_op_tables",
     "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_randomize",
-    "vsim_model_set_mode", "vsim_model_hparams", "vsim_model_eval", "vsim_model_stream",
+    "vsim_model_set_mode", "vsim_model_hparams", "vsim_model_eval", "vsim_model_eval_argmax", "vsim_model_generate",
+    "vsim_model_stream",
     "vsim_model_logits_dev", "vsim_model_info", "vsim_model_set_graph", "vsim_model_set_profile",
     "vsim_model_profile_stats", "vsim_model_free",
 ]
@@ -83,6 +84,8 @@ def lib():
     L.vsim_model_hparams.argtypes = [vp, ctypes.POINTER(HParams), ctypes.POINTER(ci), ctypes.POINTER(ci),
                                      ctypes.POINTER(ci)]
     L.vsim_model_eval.argtypes = [vp, ci, vp, ci, vp, vp, vp]
+    L.vsim_model_eval_argmax.argtypes = [vp, ci, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
+    L.vsim_model_generate.argtypes = [vp, ci, ctypes.c_int32, ci, ctypes.POINTER(ctypes.c_int32)]
     L.vsim_model_stream.restype = vp
     L.vsim_model_stream.argtypes = [vp]
     L.vsim_model_logits_dev.restype = vp
@@ -163,6 +166,18 @@ class Model:
         lg = np.zeros(self.n_vocab, np.float32) if (want_logits and self.last) else None
         check(lib().vsim_model_eval(self.h, n_past, ptr(tok), N, ptr(resid_in), ptr(resid_out), ptr(lg)), "eval")
         return lg
+
+    def eval_argmax(self, n_past, token) -> int:
+        """Greedy decode step: the next token (argmax of the logits, taken on the device)."""
+        nxt = ctypes.c_int32()
+        check(lib().vsim_model_eval_argmax(self.h, n_past, int(token), ctypes.byref(nxt)), "eval_argmax")
+        return nxt.value
+
+    def generate(self, n_past, token, n_steps) -> list:
+        """n_steps greedy decode steps kept on the device; returns the generated tokens."""
+        out = (ctypes.c_int32 * max(n_steps, 1))()
+        check(lib().vsim_model_generate(self.h, n_past, int(token), n_steps, out), "generate")
+        return list(out[:n_steps])
 
     def info(self):
         k, g, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
