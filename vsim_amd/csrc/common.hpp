@@ -83,6 +83,7 @@ struct LnQuantJob {
   // row = x + ((ja + jab) + (jf + jfb)), stored to jout when non-null
   const float *ja, *jab, *jf, *jfb;
   float *jout;
+  unsigned *clear;  // zeroed by the kernel when non-null (the layer tail's head counter)
 };
 
 struct AttnJob {
@@ -230,6 +231,8 @@ int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s);
 int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s);
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
 int launch_argmax(const float *x, int n, int *out, hipStream_t s);
+int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
+                      hipStream_t s);
 int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
 int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s);

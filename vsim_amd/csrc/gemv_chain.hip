@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "attn.hpp"
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
@@ -320,15 +321,23 @@ constexpr int C2_WAIT_VM3 = 0x0F70 | (3 * (C2_DEPTH - 2));  // wave 1: nibbles, 
 constexpr int C2_WAIT_VM2 = 0x0F70 | (2 * (C2_DEPTH - 2));  // other producers: nibbles, scales
 static_assert(3 * (C2_DEPTH - 2) < 16, "vmcnt immediate");
 
+struct C2Lds {
+  float P[C2_RING][32 * C2_LD];
+  uint4 RQ[C2_RAW][C2_NPW][64];
+  float RD[C2_RAW][C2_NPW][64];
+  float RX[C2_RAW][C2_CB * QK];
+};
+
+// tile t of the batch's jobs (blockIdx.x in k_gemv_chain32, a role offset in k_layer_tail)
 template <int DBG>
-__global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
-  __shared__ __attribute__((aligned(16))) float P[C2_RING][32 * C2_LD];
-  __shared__ __attribute__((aligned(16))) uint4 RQ[C2_RAW][C2_NPW][64];
-  __shared__ __attribute__((aligned(16))) float RD[C2_RAW][C2_NPW][64];
-  __shared__ __attribute__((aligned(16))) float RX[C2_RAW][C2_CB * QK];
+__device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds &L) {
+  auto &P = L.P;
+  auto &RQ = L.RQ;
+  auto &RD = L.RD;
+  auto &RX = L.RX;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  int t = blockIdx.x, ji = 0;
+  int ji = 0;
   while (ji < B.nj) {
     if (t < B.j[ji].w.tiles) break;
     t -= B.j[ji].w.tiles;
@@ -629,6 +638,78 @@ __global__ void __launch_bounds__(C3_THREADS, 1) k_gemv_chain2(GemvBatch B) {
   } else if (row < rows) {
     y[row] = bias ? acc + bias[row] : acc;
   }
+}
+
+template <int DBG>
+__global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
+  __shared__ C2Lds L;
+  chain32_body<DBG>(B, blockIdx.x, L);
+}
+
+// ================================================================== fused layer tail
+// fc_out, the attention heads and the out-projection of one layer in one launch, so the
+// attention and the out-projection run beside fc_out, whose K = 4E chain is the layer's
+// longest dependency, instead of before it.  Roles by workgroup index:
+//   [0, nf)          fc_out tiles (32-row chain GEMV)
+//   [nf, nf + H)     attention heads (attn.hpp with this kernel's 5 waves); each head
+//                    releases its output and counts itself in *done (agent scope)
+//   [nf + H, ...)    out-projection tiles; wait until *done == H, then acquire
+// Waiting workgroups only wait for lower-indexed ones, which the dispatcher has already
+// placed, so the wait always ends.  *done is zeroed by the layer's LayerNorm kernel.
+struct TailJob {
+  GemvBatch f, o;
+  AttnJob a;
+  unsigned *done;
+  int nf;
+};
+
+__global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
+  __shared__ union {
+    C2Lds g;
+    float a[sizeof(C2Lds) / sizeof(float)];
+  } L;
+  int b = blockIdx.x;
+  if (b < T.nf) {
+    chain32_body<0>(T.f, b, L.g);
+    return;
+  }
+  b -= T.nf;
+  if (b < T.a.H) {
+    attn_body<C2_THREADS>(T.a, b, L.a);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's output stores
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  b -= T.a.H;
+  if (threadIdx.x == 0)
+    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)T.a.H)
+      __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  chain32_body<0>(T.o, b, L.g);
+}
+
+int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
+                      hipStream_t s) {
+  if (a.d % 32 != 0 || a.d > 64 * ATT_DPL || (size_t)(2 * a.d + n_ctx) * sizeof(float) > sizeof(C2Lds)) {
+    set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
+    return VSIM_EINVAL;
+  }
+  TailJob T;
+  T.f = f;
+  T.o = o;
+  T.a = a;
+  T.done = done;
+  T.nf = 0;
+  for (int i = 0; i < f.nj; ++i) T.nf += f.j[i].w.tiles;
+  int no = 0;
+  for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;
+  // dynamic LDS pad: above half the CU's LDS, so one workgroup per CU (fc_out's consumer
+  // keeps its SIMD); the out-projection tiles that find no CU start as attention heads end
+  hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H + no), dim3(C2_THREADS), 8192, s, T);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
 }
 
 // ================================================================== 64-row, SIMD0 solo

@@ -90,6 +90,7 @@ struct vsim_model {
   hipGraphExec_t gexec_gen = nullptr;
   int graph_gen_mode = -1;
   int *hist_dev = nullptr;
+  unsigned *tail_done = nullptr;  // attention heads finished in the fused layer tail
   // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
   // fc_out, whose K = 4E chain is the layer's critical path
   hipStream_t stream2 = nullptr;
@@ -129,6 +130,8 @@ void free_scratch(vsim_model *m) {
   if (m->gexec_gen) (void)hipGraphExecDestroy(m->gexec_gen);
   if (m->graph_gen) (void)hipGraphDestroy(m->graph_gen);
   if (m->hist_dev) (void)hipFree(m->hist_dev);
+  if (m->tail_done) (void)hipFree(m->tail_done);
+  m->tail_done = nullptr;
   m->gexec_gen = nullptr;
   m->graph_gen = nullptr;
   m->graph_gen_mode = -1;
@@ -192,6 +195,8 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMalloc((void **)&m->am_dev, sizeof(int)));
   VSIM_HIP(hipHostMalloc((void **)&m->am_host, sizeof(int), hipHostMallocDefault));
   VSIM_HIP(hipMalloc((void **)&m->hist_dev, (size_t)m->n_ctx * sizeof(int)));
+  VSIM_HIP(hipMalloc((void **)&m->tail_done, sizeof(unsigned)));
+  VSIM_HIP(hipMemset(m->tail_done, 0, sizeof(unsigned)));
   m->n_max = n;
   return VSIM_OK;
 }
@@ -423,6 +428,11 @@ int enqueue_decode(vsim_model *m, int &nk) {
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
   const bool gptj = m->arch == VSIM_ARCH_GPTJ;
   hipStream_t s = m->stream;
+  // fc_out, attention and out-projection as one launch (k_layer_tail); VSIM_TAIL=0: separate
+  static const bool tail_env = [] {
+    const char *e = getenv("VSIM_TAIL");
+    return !(e && e[0] == '0');
+  }();
   // VSIM_SPLIT=1: the attention branch on a second stream beside fc_out.  Measured slower
   // (413 vs 442 tok/s, GPT-J): each cross-queue event wait costs 4-10 us, more than the
   // overlap wins.  Kept for A/B timing.
@@ -466,6 +476,9 @@ int enqueue_decode(vsim_model *m, int &nk) {
       join_into(j1, true);
       join_into(j2, false);
     }
+    const bool tail = tail_env && !split && m->mode == VSIM_MODE_EXACT &&
+                      (size_t)(2 * d + m->n_ctx) * sizeof(float) <= 75264;
+    if (tail) j1.clear = m->tail_done;
     RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
     ++nk;
     if (pending) cur ^= 1;
@@ -533,6 +546,21 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.oq_d = da;
     A.oxd = m->xda;
     A.out = nullptr;
+    if (tail) {
+      GemvBatch Bf{}, Bo{};
+      Bf.nj = 1;
+      job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
+      Bo.nj = 1;
+      job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
+      ev = prof_begin(m);
+      RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
+      prof_end(m, ev, w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w));
+      ++nk;
+      pending = true;
+      pend_ab = gptj ? nullptr : L.bo;
+      pend_fb = L.bproj;
+      continue;
+    }
     RC(launch_attn_decode(A, m->n_ctx, sa));
     ++nk;
     // {fc_out, out-projection} without biases (they join in the next norm)
