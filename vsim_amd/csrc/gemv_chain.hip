@@ -959,7 +959,12 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
       const char *e = getenv("VSIM_SOLO_PF");
       return e ? atoi(e) : 3;
     }();
-#define C5L(D, CB, PF) hipLaunchKernelGGL((k_gemv_solo<D, CB, PF>), dim3(groups), dim3(64 * SoloShape<CB>::WAVES), 0, s, B)
+    static const size_t solo_pad = [] {  // VSIM_SOLO_PAD=bytes: dynamic LDS pad (occupancy experiments)
+      const char *e = getenv("VSIM_SOLO_PAD");
+      return e ? (size_t)atol(e) : (size_t)0;
+    }();
+#define C5L(D, CB, PF) \
+  hipLaunchKernelGGL((k_gemv_solo<D, CB, PF>), dim3(groups), dim3(64 * SoloShape<CB>::WAVES), solo_pad, s, B)
     if (solo_cb == 9) {
       if (pf == 7) C5L(0, 9, 7); else C5L(0, 9, 3);
     } else {

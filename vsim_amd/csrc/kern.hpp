@@ -152,7 +152,9 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
                                const float *__restrict__ gb, unsigned *stats, const float *__restrict__ ja = nullptr,
                                const float *__restrict__ jab = nullptr, const float *__restrict__ jf = nullptr,
                                const float *__restrict__ jfb = nullptr, float *__restrict__ jout = nullptr,
-                               unsigned long long *prof = nullptr) {
+                               unsigned long long *prof = nullptr, int s0 = 0, int s1 = 1 << 30) {
+  // [s0, s1): the float4 slice of the row this workgroup normalizes (and writes to jout);
+  // the statistics always cover the whole row
   constexpr int NW = NT / 64;
   // timing experiment (prof != null): phase stamps of thread 0
   auto stamp = [&](int i) {
@@ -169,23 +171,18 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   double s = 0.0, sa = 0.0;
   int um = 1 << 30;
   // affine factors of this thread's first float4, loaded up front (used in the last pass)
+  const int i0 = max(s0, 0) + (int)threadIdx.x;  // this thread's first float4 of the slice
   float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), b0 = w0;
-  if (gw && (int)threadIdx.x < n4) {
-    w0 = ((const float4 *)gw)[threadIdx.x];
-    b0 = ((const float4 *)gb)[threadIdx.x];
+  if (gw && i0 < min(s1, n4)) {
+    w0 = ((const float4 *)gw)[i0];
+    b0 = ((const float4 *)gb)[i0];
   }
-  for (int i = threadIdx.x; i < n4; i += NT) {
-    float4 v = ((const float4 *)x)[i];
+  auto join = [&](int i, float4 v, float4 a, float4 ab, float4 f, float4 fb) {
     if (ja) {
-      float4 a = ((const float4 *)ja)[i];
-      const float4 f = ((const float4 *)jf)[i], fb = ((const float4 *)jfb)[i];
-      if (jab) {
-        const float4 ab = ((const float4 *)jab)[i];
-        a = make_float4(a.x + ab.x, a.y + ab.y, a.z + ab.z, a.w + ab.w);
-      }
+      if (jab) a = make_float4(a.x + ab.x, a.y + ab.y, a.z + ab.z, a.w + ab.w);
       v = make_float4(v.x + (a.x + (f.x + fb.x)), v.y + (a.y + (f.y + fb.y)), v.z + (a.z + (f.z + fb.z)),
                       v.w + (a.w + (f.w + fb.w)));
-      if (jout) ((float4 *)jout)[i] = v;
+      if (jout && i >= s0 && i < s1) ((float4 *)jout)[i] = v;
     }
     ((float4 *)row)[i] = v;
     const float e[4] = {v.x, v.y, v.z, v.w};
@@ -195,6 +192,32 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
       sa += (double)fabsf(e[j]);
       um = min(um, ulp_exp(e[j]));
     }
+  };
+  auto ld4 = [](const float *p, int i) {
+    return p ? ((const float4 *)p)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  constexpr int UP = 4;  // rows up to UP * NT float4: every load issued before any arithmetic
+  if (n4 <= UP * NT) {
+    float4 v[UP], a[UP], ab[UP], f[UP], fb[UP];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int i = (int)threadIdx.x + u * NT;
+      if (i < n4) {
+        v[u] = ((const float4 *)x)[i];
+        a[u] = ld4(ja, i);
+        ab[u] = ld4(jab, i);
+        f[u] = ld4(jf, i);
+        fb[u] = ld4(jfb, i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int i = (int)threadIdx.x + u * NT;
+      if (i < n4) join(i, v[u], a[u], ab[u], f[u], fb[u]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < n4; i += NT)
+      join(i, ((const float4 *)x)[i], ld4(ja, i), ld4(jab, i), ld4(jf, i), ld4(jfb, i));
   }
   stamp(1);
   s = wave_sum_d(s);
@@ -271,11 +294,11 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     scale = bcast_f;
   }
   stamp(4);
-  for (int i = threadIdx.x; i < n4; i += NT) {
+  for (int i = max(s0, 0) + (int)threadIdx.x; i < min(s1, n4); i += NT) {
     const float4 v4 = ((const float4 *)row)[i];
     float e[4] = {v4.x, v4.y, v4.z, v4.w};
     float4 w4 = w0, b4 = b0;
-    if (gw && i != (int)threadIdx.x) {
+    if (gw && i != i0) {
       w4 = ((const float4 *)gw)[i];
       b4 = ((const float4 *)gb)[i];
     }

@@ -27,20 +27,27 @@ extern unsigned *g_norm_stats;
 // ------------------------------------------------------------------ 1. LN + quantize
 // One 1024-thread workgroup per LayerNorm (two for GPT-NeoX's parallel-residual pair); the
 // normalized row is quantized by whole waves, two 32-blocks per wave step.
-constexpr int LNQ_THREADS = 1024;
+constexpr int LNQ_THREADS = 512;
 __device__ unsigned long long g_ln_prof[8];  // timing experiment output (VSIM_LN_DBG)
 
+// LNQ_SPLIT workgroups per LayerNorm: each computes the whole row's statistics (the row is
+// 16 KB, read from L2) and normalizes, writes and quantizes one slice of LNQ_SPLIT, so the
+// latency-bound per-element phases run on LNQ_SPLIT CUs.
+constexpr int LNQ_SPLIT = 8;
 template <bool PROF>
 __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float row[];
-  const LnQuantJob &J = blockIdx.x == 0 ? j0 : j1;
+  const int part = blockIdx.x % LNQ_SPLIT;
+  const LnQuantJob &J = blockIdx.x < LNQ_SPLIT ? j0 : j1;
   unsigned long long *prof = PROF && blockIdx.x == 0 ? g_ln_prof : nullptr;
-  if (J.clear && threadIdx.x == 0) *J.clear = 0u;
-  ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, stats, J.ja, J.jab, J.jf, J.jfb, J.jout, prof);
+  if (J.clear && blockIdx.x == 0 && threadIdx.x == 0) *J.clear = 0u;
   const int nb = n / QK, lane = threadIdx.x & 63;
-  for (int b2 = threadIdx.x >> 6; 2 * b2 < nb; b2 += LNQ_THREADS / 64) {
-    const int b = 2 * b2 + (lane >> 5);
-    const bool ok = b < nb;
+  const int b0 = part * nb / LNQ_SPLIT, b1 = (part + 1) * nb / LNQ_SPLIT;  // this slice's blocks
+  ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, part == 0 ? stats : nullptr, J.ja, J.jab, J.jf, J.jfb, J.jout,
+                              prof, b0 * QK / 4, b1 * QK / 4);
+  for (int b2 = threadIdx.x >> 6; b0 + 2 * b2 < b1; b2 += LNQ_THREADS / 64) {
+    const int b = b0 + 2 * b2 + (lane >> 5);
+    const bool ok = b < b1;
     const float v = ok ? row[b * QK + (lane & 31)] : 0.0f;
     quantize_half(v, lane, ok, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
   }
@@ -49,12 +56,13 @@ __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuant
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
   static const bool prof = getenv("VSIM_LN_DBG") != nullptr;
+  const dim3 grid((j1 ? 2 : 1) * LNQ_SPLIT);
   if (prof)
-    hipLaunchKernelGGL(k_ln_quant<true>, dim3(j1 ? 2 : 1), dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0,
-                       n, g_norm_stats);
+    hipLaunchKernelGGL(k_ln_quant<true>, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
+                       g_norm_stats);
   else
-    hipLaunchKernelGGL(k_ln_quant<false>, dim3(j1 ? 2 : 1), dim3(LNQ_THREADS), (size_t)n * 4, s, j0,
-                       j1 ? *j1 : j0, n, g_norm_stats);
+    hipLaunchKernelGGL(k_ln_quant<false>, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
+                       g_norm_stats);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
