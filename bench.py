@@ -37,7 +37,9 @@ from vsim_amd import pipeline  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s measured copy
 PROMPT = [50278, 12092, 2, 0, 50281]
-GEMV_KERNELS = ("k_gemv_chain", "k_gemv_fast")  # name prefixes of the Q4_0 GEMV launches
+# name parts of the Q4_0 GEMV launches (k_layer_tail: fc_out + out-projection, with the
+# attention heads running beside them in the same launch)
+GEMV_KERNELS = ("k_gemv_chain", "k_gemv_solo", "k_layer_tail", "k_gemv_fast")
 # HBM traffic of the GEMV launches, from a separate `rocprofv3 --pmc FETCH_SIZE` pass of this
 # bench (tools/profile_round.sh) committed under profiles/; FETCH_SIZE is in KiB and reads
 # half of the bytes of a 16-byte-per-lane streaming read on gfx950 (MI355X_MICROARCH.md,
@@ -320,7 +322,7 @@ def main():
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4),
                         "traffic": round(traffic) if traffic else None,
-                        "kernel": "k_gemv_chain*" if args.mode == "exact" else "k_gemv_fast*",
+                        "kernel": "k_gemv_solo/k_layer_tail/k_gemv_chain32" if args.mode == "exact" else "k_gemv_fast*",
                         "bytes_per_launch": round(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 3),
                         "launches": prof["gemv_launches"],
                         "gemv_share_of_step": round(prof["gemv_ms"] / 1e3 / prof_wall, 4),
