@@ -225,6 +225,47 @@ def run_pipeline(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def run_prefill(args, dev):
+    """One prompt eval of args.prefill tokens (codegen-16B, N = 2048) in
+    fast mode: every Q4_0 matmul on the fp16 MFMA GEMM after in-LDS dequant
+    (gemm_f16.hip); attention and the elementwise ops on the general-path kernels."""
+    import torch
+    arch_s, hp = mg.CONFIGS[args.config]
+    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    N = args.prefill
+    model = hip.Model.create(arch, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
+                                        n_layer=hp.n_layer, n_rot=hp.n_rot,
+                                        use_parallel_residual=hp.use_parallel_residual),
+                             n_ctx=N + 8, device=dev)
+    model.randomize(seed=1234, std=0.02)
+    model.set_mode(hip.MODE_FAST)
+    ids = [(7919 * i + 11) % hp.n_vocab for i in range(N)]
+    model.eval(0, ids)  # warm-up (allocates the N-token scratch)
+    torch.cuda.synchronize()
+    reps = max(1, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        model.eval(0, ids)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    E, F, L, V = hp.n_embd, hp.n_ff, hp.n_layer, hp.n_vocab
+    # flops as computed: every layer matmul over N tokens, the head for the last row (the
+    # logits that leave the eval, vsim.cpp:736-737), causal QK^T and PV
+    gemm_flops = 2.0 * N * L * (4 * E * E + 2 * E * F) + 2.0 * V * E
+    attn_flops = 2.0 * 2.0 * L * E * (N * (N + 1) / 2.0)
+    tflops = (gemm_flops + attn_flops) / dt / 1e12
+    print(json.dumps({
+        "metric": f"prefill tokens/s {args.config} Q4_0 seq={N} @1 GPU (fp16 MFMA dequant-GEMM)",
+        "value": round(N / dt, 1), "unit": "tokens/s", "n_gpus": 1, "steps": reps,
+        "ms_per_prompt": round(dt * 1e3, 2), "higher_is_better": True,
+        "dtype": "f16 MFMA, f32 accumulate", "data": "synthetic (random-init weights, drawn on device)",
+        "config": {"workload": f"{args.config} prompt eval, N={N}", "mode": "fast"},
+        "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": 2500.0, "unit": "TFLOP/s",
+                     "frac": round(tflops / 2500.0, 4), "traffic": None,
+                     "flops": {"gemm": gemm_flops, "attention": attn_flops}},
+    }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,6 +280,8 @@ def main():
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-mode companion measurement")
     ap.add_argument("--pipeline", action="store_true",
                     help="split the layers over the ranks (one residual send per stage boundary per token)")
+    ap.add_argument("--prefill", type=int, default=0,
+                    help="time one prompt eval of this many tokens instead of decode (fast-mode fp16 MFMA GEMM)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: host-staged sends, for rehearsing the pipeline with ranks sharing a GPU")
     args = ap.parse_args()
@@ -258,6 +301,9 @@ def main():
             dist.init_process_group("gloo")
     if args.pipeline:
         run_pipeline(args, world, rank, dev, dist)
+        return
+    if args.prefill:
+        run_prefill(args, dev)
         return
 
     arch_s, hp = mg.CONFIGS[args.config]

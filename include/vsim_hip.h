@@ -108,6 +108,11 @@ int vsim_op_rope(int style, float *x, int d, int H, int T, int n_past, int n_dim
 int vsim_op_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq,
                void *stream);
 int vsim_op_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, void *stream);
+/* Fast-mode prompt attention (fp16 MFMA, one pass with an online softmax): for N queries
+ * Q [N][d*H] at positions n_past.., keys/values kc/vc [n_past+N][d*H] (post-RoPE K),
+ * out[q][h*d + dd] = softmax_k(scale * K.Q, causal) . V.  d in {64, 96, 128, 256}. */
+int vsim_op_attn_prefill(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
+                         float scale, float *out, void *stream);
 /* device fp16 tables (exp, gelu) as built by ggml_init (ggml.c:1240-1251) */
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host);
 

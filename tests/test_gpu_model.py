@@ -199,3 +199,21 @@ def test_generate_matches_stepwise_greedy(graph, tmp_path):
     got = b.generate(len(prompt), tok, 10)  # in two calls: the loop resumes from (n_past, token)
     got += b.generate(len(prompt) + 10, got[-1], 6)
     assert got == ref
+
+
+def test_fast_prefill_tracks_exact(tmp_path):
+    """A 40-token prompt in fast mode runs the fp16 MFMA GEMM and attention (N >= 8); its
+    last-row logits stay close to exact mode's (the fast path is not bit-exact: cos > 0.95,
+    the same bound as the decode fast mode)."""
+    arch_s, hp = mg.CONFIGS["small-gptj"]
+    path = str(tmp_path / "pf.bin")
+    mg.write_model(path, arch_s, hp, seed=3, std=0.05)
+    ids = [(37 * i + 5) % hp.n_vocab for i in range(40)]
+    me = hip.Model.load(path, hip.ARCH_GPTJ)
+    me.set_mode(hip.MODE_EXACT)
+    le = me.eval(0, ids)
+    mf = hip.Model.load(path, hip.ARCH_GPTJ)
+    mf.set_mode(hip.MODE_FAST)
+    lf = mf.eval(0, ids)
+    cos = float(np.dot(le, lf) / (np.linalg.norm(le) * np.linalg.norm(lf)))
+    assert cos > 0.95, cos

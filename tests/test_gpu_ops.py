@@ -213,3 +213,58 @@ def test_gemv_exact_full_width_vs_oracle(M, K):
     w = repack(aos, M, K)
     xq, xd = quantize(x, K, 1)
     assert np.array_equal(bits(gemv(w, M, K, xq, xd, 1, hip.MODE_EXACT)), bits(ref))
+
+
+@pytest.mark.parametrize("M,K,N", [(520, 512, 300), (256, 4096, 8), (1000, 1024, 129), (96, 96, 40)])
+def test_prefill_gemm_f16(M, K, N):
+    """Fast-mode prompt GEMM (gemm_f16.hip: fp16 MFMA after in-LDS dequant).  Operands are
+    d*(q-8) rounded once to fp16, products exact, fp32 accumulation: the result must be
+    within 4*K*2^-24*sum|w16*x16| of the fp64 product of the fp16-rounded operands, and
+    within 2^-10*sum|w*x| (operand rounding) of the unrounded Q4_0 x Q4_0 product.
+    Ragged M and N (not multiples of the 128 x 128 tile) and K = 96 (odd block count)."""
+    rng = np.random.default_rng(M + K + N)
+    w_aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05))
+    b = rng.standard_normal(M).astype(np.float32)
+    w = repack(w_aos, M, K)
+    xq, xd = quantize(rng.standard_normal(N * K).astype(np.float32), K, N)
+    y = gemv(w, M, K, xq, xd, N, hip.MODE_FAST, bias=dev(b)).reshape(N, M)
+    xq_aos = torch.empty(N * K // 32 * 20, dtype=torch.uint8, device=DEV)
+    hip.check(hip.lib().vsim_op_act_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
+    W = mg.dequantize_q4_0(w_aos, K)
+    X = mg.dequantize_q4_0(host(xq_aos), K)
+    W16 = W.astype(np.float16).astype(np.float64)
+    X16 = X.astype(np.float16).astype(np.float64)
+    ref16 = X16 @ W16.T + b
+    abs16 = np.abs(X16) @ np.abs(W16).T
+    assert np.all(np.abs(y - ref16) <= 4.0 * K * 2.0 ** -24 * abs16 + 1e-6 * np.abs(b))
+    ref = X.astype(np.float64) @ W.astype(np.float64).T + b
+    absum = np.abs(X.astype(np.float64)) @ np.abs(W.astype(np.float64)).T
+    assert np.all(np.abs(y - ref) <= 2.0 ** -10 * absum + 1e-5 * (np.abs(b) + 1))
+
+
+@pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])
+def test_attn_prefill_f16(d, H, N, n_past):
+    """Fast-mode prompt attention (attn_prefill.hip) against fp64 causal attention:
+    scores and probabilities pass through fp16, so the tolerance is 2e-2 of max|V| (the
+    observed error is ~1e-3)."""
+    rng = np.random.default_rng(d + N + n_past)
+    E, nk = d * H, n_past + N
+    Q = rng.standard_normal((N, E)).astype(np.float32)
+    K = rng.standard_normal((nk, E)).astype(np.float32)
+    V = rng.standard_normal((nk, E)).astype(np.float32)
+    scale = float(np.float32(1.0 / np.sqrt(d)))
+    out = torch.empty(N * E, dtype=torch.float32, device=DEV)
+    q_, k_, v_ = dev(Q), dev(K), dev(V)
+    hip.check(hip.lib().vsim_op_attn_prefill(q_.data_ptr(), k_.data_ptr(), v_.data_ptr(), d, H, N, n_past, scale,
+                                             out.data_ptr(), None), "attn_prefill")
+    y = host(out).reshape(N, E)
+    ref = np.empty((N, E))
+    for h in range(H):
+        sl = slice(h * d, (h + 1) * d)
+        s = (Q[:, sl].astype(np.float64) @ K[:, sl].astype(np.float64).T) * scale
+        mask = np.arange(nk)[None, :] > (n_past + np.arange(N))[:, None]
+        s[mask] = -np.inf
+        p = np.exp(s - s.max(axis=1, keepdims=True))
+        p /= p.sum(axis=1, keepdims=True)
+        ref[:, sl] = p @ V[:, sl].astype(np.float64)
+    assert np.max(np.abs(y - ref)) <= 2e-2 * np.max(np.abs(V))

@@ -83,6 +83,10 @@ int vsim_op_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, i
 int vsim_op_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, void *stream) {
   return launch_kqv(V, ldv, S, d, H, nk, n, out, 0, (hipStream_t)stream);
 }
+int vsim_op_attn_prefill(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
+                         float scale, float *out, void *stream) {
+  return launch_attn_prefill_f16(Q, kc, vc, d, H, N, n_past, scale, out, (hipStream_t)stream);
+}
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host) { return tables_host(exp_f16_host, gelu_f16_host); }
 
 }  // extern "C"

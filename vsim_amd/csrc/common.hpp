@@ -231,6 +231,10 @@ int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s);
 int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s);
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
 int launch_argmax(const float *x, int n, int *out, hipStream_t s);
+int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s);
+bool attn_prefill_supported(int d);
+int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
+                            float scale, float *out, hipStream_t s);
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
                       hipStream_t s);
 int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);

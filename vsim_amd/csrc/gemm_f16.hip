@@ -1,0 +1,176 @@
+// vsim_amd/csrc/gemm_f16.hip — prompt (prefill) GEMM on fp16 MFMA after in-LDS dequant.
+//
+// Y[n][m] (+ bias[m]) = sum_k W[m][k] * X[n][k] for N prompt tokens at once, the shape of
+// ggml_compute_forward_mul_mat_q4_0_f32 (ggml.c:4891-5165) with N > 1: W is the Q4_0
+// weight in the W4T32 layout, X the Q4_0-quantized activation rows the reference's INIT
+// phase produces (ggml.c:5024-5041; Q4 SoA here).  Both are dequantized to fp16 while
+// they are staged into LDS (d*(q-8) rounded once to fp16), multiplied on
+// v_mfma_f32_32x32x16_f16 and accumulated in fp32.
+//
+// Numerics: this is the throughput path for long prompts (codegen-16B, N = 2048); it is
+// not the reference's sequential fp32 chain per (row, token), so it belongs to the fast
+// mode.  Exact mode keeps the per-chain kernel for prompt batches.
+//
+// Tiling: one workgroup = 128 weight rows x 128 tokens, 4 waves of 64 x 64 (2 x 2 MFMA
+// tiles of 32 x 32); K in steps of 64 (two Q4_0 blocks).  Staging: each of the 256 threads
+// dequantizes one (row, block) unit of W and one of X per step -- 16 bytes of nibbles and
+// a scale into 32 halves -- with the fp8 nibble conversion of the exact GEMV (an e4m3 byte
+// n in 0..15 is n * 2^-9).  The next step's units are loaded into registers before the
+// MFMAs of the current step, so their global latency hides behind the matrix work.
+#include "kern.hpp"
+#include "../../include/vsim_hip.h"
+
+namespace vsim {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int GM_BM = 128, GM_BN = 128, GM_BK = 64, GM_THREADS = 256;
+constexpr int GM_LD = GM_BK + 8;  // halves per LDS row: 16-byte pad against bank conflicts
+
+// 32 fp16 values d * (q - 8) of one Q4_0 block (byte j: element 2j low nibble, 2j+1 high)
+__device__ __forceinline__ void deq_block_f16(uint4 q, float d, half8 out[4]) {
+  const f32x2 d2 = {512.0f * d, 512.0f * d}, m2 = {-8.0f * d, -8.0f * d};
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int lo = (int)(qw[w] & 0x0F0F0F0Fu), hi = (int)((qw[w] >> 4) & 0x0F0F0F0Fu);
+    // elements 8w .. 8w+7: (lo b0, hi b0, lo b1, hi b1, lo b2, hi b2, lo b3, hi b3)
+    const f32x2 l01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, false), d2, m2);
+    const f32x2 h01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, false), d2, m2);
+    const f32x2 l23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, true), d2, m2);
+    const f32x2 h23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, true), d2, m2);
+    half8 h;
+    h[0] = (_Float16)l01.x;
+    h[1] = (_Float16)h01.x;
+    h[2] = (_Float16)l01.y;
+    h[3] = (_Float16)h01.y;
+    h[4] = (_Float16)l23.x;
+    h[5] = (_Float16)h23.x;
+    h[6] = (_Float16)l23.y;
+    h[7] = (_Float16)h23.y;
+    out[w] = h;
+  }
+}
+
+__global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const uint8_t *__restrict__ xqs,
+                                                             const float *__restrict__ xdd, int N,
+                                                             const float *__restrict__ bias, float *__restrict__ Y) {
+  __shared__ __attribute__((aligned(16))) _Float16 As[GM_BM * GM_LD];
+  __shared__ __attribute__((aligned(16))) _Float16 Bs[GM_BN * GM_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = W.rows, nb = W.k / QK;
+  const int m0 = blockIdx.x * GM_BM, n0 = blockIdx.y * GM_BN;
+  // staging unit of this thread: row (of W) / token (of X) u, block ub of the K step
+  const int u = tid & 127, ub = tid >> 7;
+  const int mrow = m0 + u, ntok = n0 + u;
+  const bool mok = mrow < M, nok = ntok < N;
+  const size_t wbase = mok ? ((size_t)(mrow / T32) * nb * T32 + (mrow & (T32 - 1))) : 0;
+  auto ldW = [&](int kb, uint4 &q, float &d) {  // block kb of row mrow
+    const int b = kb + ub;
+    if (mok && b < nb) {
+      const size_t o = wbase + (size_t)b * T32;
+      q = *(const uint4 *)(W.qs + o * 16);
+      d = W.d[o];
+    } else {
+      q = make_uint4(0x88888888u, 0x88888888u, 0x88888888u, 0x88888888u);  // q = 8: value 0
+      d = 0.0f;
+    }
+  };
+  auto ldX = [&](int kb, uint4 &q, float &d) {
+    const int b = kb + ub;
+    if (nok && b < nb) {
+      const size_t o = (size_t)ntok * nb + b;
+      q = *(const uint4 *)(xqs + o * 16);
+      d = xdd[o];
+    } else {
+      q = make_uint4(0x88888888u, 0x88888888u, 0x88888888u, 0x88888888u);
+      d = 0.0f;
+    }
+  };
+  const int wm = wave & 1, wn = wave >> 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+  uint4 qa, qb;
+  float da, db;
+  ldW(0, qa, da);
+  ldX(0, qb, db);
+  const int r = lane & 31, h = lane >> 5;
+  for (int kb = 0; kb < nb; kb += 2) {
+    // dequantize this step's units into LDS
+    half8 ha[4], hb[4];
+    deq_block_f16(qa, da, ha);
+    deq_block_f16(qb, db, hb);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      *(half8 *)&As[u * GM_LD + ub * 32 + 8 * w] = ha[w];
+      *(half8 *)&Bs[u * GM_LD + ub * 32 + 8 * w] = hb[w];
+    }
+    __syncthreads();
+    // next step's units in flight during the MFMAs
+    if (kb + 2 < nb) {
+      ldW(kb + 2, qa, da);
+      ldX(kb + 2, qb, db);
+    }
+#pragma unroll
+    for (int kk = 0; kk < GM_BK / 16; ++kk) {
+      half8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *(const half8 *)&As[(wm * 64 + i * 32 + r) * GM_LD + kk * 16 + 8 * h];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = *(const half8 *)&Bs[(wn * 64 + j * 32 + r) * GM_LD + kk * 16 + 8 * h];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C/D map of 32x32 MFMA: column (token) = lane & 31, row (weight row) =
+  // (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + r;
+      if (n >= N) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int m = m0 + wm * 64 + i * 32 + 8 * g + 4 * h;
+        float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        if (bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (m + e < M) v[e] = v[e] + bias[m + e];
+        }
+        float *dst = Y + (size_t)n * M + m;
+        if (m + 3 < M && (M & 3) == 0) {
+          *(float4 *)dst = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (m + e < M) dst[e] = v[e];
+        }
+      }
+    }
+}
+
+int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s) {
+  if (W.k % QK) {
+    set_error("q4 gemm: K must be a multiple of 32");
+    return VSIM_EINVAL;
+  }
+  const size_t nbk = (size_t)n * (W.k / QK);
+  const uint8_t *xqs = (const uint8_t *)xq;
+  const float *xdd = (const float *)(xqs + nbk * 16);
+  const dim3 grid((W.rows + GM_BM - 1) / GM_BM, (n + GM_BN - 1) / GM_BN);
+  hipLaunchKernelGGL(k_gemm_q4_f16, grid, dim3(GM_THREADS), 0, s, W, xqs, xdd, n, bias, y);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+}  // namespace vsim

@@ -370,9 +370,14 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
-  RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
-  RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
-  RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
+  if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
+    // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
+    RC(launch_attn_prefill_f16(m->Qb, kc, vc, d, H, N, n_past, scale, m->attn_in, s)); ++nk;
+  } else {
+    RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
+    RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
+    RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
+  }
   RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, gptj ? nullptr : L.bo, m->attn, nk));
   // feed-forward input
   const uint8_t *fxq = m->xq1;

@@ -244,11 +244,15 @@ int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
   return VSIM_OK;
 }
 
+constexpr int GEMM_MIN_N = 8;  // fast mode: from this many tokens on, the MFMA GEMM
+
 int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias, float *y,
                    int mode, hipStream_t s) {
   if (K % QK || M <= 0 || n <= 0) { set_error("q4_gemv: bad shape"); return VSIM_EINVAL; }
   const W4 W = w4_view(w, M, K);
   if (mode == VSIM_MODE_EXACT && !xd) { set_error("q4_gemv: exact mode needs xd"); return VSIM_EINVAL; }
+  // fast mode, prompt batches: fp16 MFMA GEMM after in-LDS dequant (gemm_f16.hip)
+  if (mode == VSIM_MODE_FAST && n >= GEMM_MIN_N) return launch_gemm_q4_f16(W, xq, n, bias, y, s);
   if (mode == VSIM_MODE_EXACT && n > 1) {
     hipLaunchKernelGGL(k_gemv_exact_rows, dim3((M + 255) / 256, n), dim3(256), 0, s, W, xd, n, bias, y);
     VSIM_HIP(hipGetLastError());

@@ -29,6 +29,7 @@ EXPORTS = [
     "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_act_repack", "vsim_op_act_unpack",
     "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_get_rows",
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
+    "vsim_op_attn_prefill",
     "vsim_op_tables",
     "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_randomize",
     "vsim_model_set_mode", "vsim_model_hparams", "vsim_model_eval", "vsim_model_eval_argmax", "vsim_model_generate",
@@ -74,6 +75,7 @@ def lib():
     L.vsim_op_rope.argtypes = [ci, vp, ci, ci, ci, ci, ci, ci, vp]
     L.vsim_op_kq.argtypes = [vp, ci, vp, ci, ci, ci, ci, ci, vp, vp]
     L.vsim_op_kqv.argtypes = [vp, ci, vp, ci, ci, ci, ci, vp, vp]
+    L.vsim_op_attn_prefill.argtypes = [vp, vp, vp, ci, ci, ci, ci, cf, vp, vp]
     L.vsim_op_tables.argtypes = [vp, vp]
     L.vsim_model_create.argtypes = [ci, ctypes.POINTER(HParams), ci, ci, ci, ci, ctypes.POINTER(vp)]
     L.vsim_model_load_file.argtypes = [ctypes.c_char_p, ci, ci, ci, ci, ci, ctypes.POINTER(vp)]
