@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "fast.hpp"
 #include "../../include/vsim_hip.h"
 
 using namespace vsim;
@@ -91,6 +92,10 @@ struct vsim_model {
   int graph_gen_mode = -1;
   int *hist_dev = nullptr;
   unsigned *tail_done = nullptr;  // attention heads finished in the fused layer tail
+  // fast-mode decode step (fast_decode.hip): fc_out split-K partial rows and attention
+  // chunk partials (both consumed by the layer's k_fast_oproj_join)
+  float *fast_ffp = nullptr, *fast_part = nullptr;
+
   // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
   // fc_out, whose K = 4E chain is the layer's critical path
   hipStream_t stream2 = nullptr;
@@ -132,6 +137,9 @@ void free_scratch(vsim_model *m) {
   if (m->hist_dev) (void)hipFree(m->hist_dev);
   if (m->tail_done) (void)hipFree(m->tail_done);
   m->tail_done = nullptr;
+  if (m->fast_ffp) (void)hipFree(m->fast_ffp);
+  if (m->fast_part) (void)hipFree(m->fast_part);
+  m->fast_ffp = m->fast_part = nullptr;
   m->gexec_gen = nullptr;
   m->graph_gen = nullptr;
   m->graph_gen_mode = -1;
@@ -197,6 +205,12 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMalloc((void **)&m->hist_dev, (size_t)m->n_ctx * sizeof(int)));
   VSIM_HIP(hipMalloc((void **)&m->tail_done, sizeof(unsigned)));
   VSIM_HIP(hipMemset(m->tail_done, 0, sizeof(unsigned)));
+  {
+    const size_t d = E / H, nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
+    VSIM_HIP(fa(&m->fast_ffp, FD_SF * E));
+    VSIM_HIP(fa(&m->fast_part, H * nch * (d + 2)));
+    VSIM_HIP(hipMemset(m->fast_part, 0, H * nch * (d + 2) * sizeof(float)));  // finite stale values
+  }
   m->n_max = n;
   return VSIM_OK;
 }
@@ -427,9 +441,147 @@ void prof_end(vsim_model *m, hipEvent_t *ev, double bytes, hipStream_t st = null
 
 double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 
+// Fast-mode single-token step (fast_decode.hip): 3 launches per layer.  Same buffers and
+// the same replayable form as enqueue_decode (token and n_past from device memory).
+// Shapes the fast step handles: head dim a multiple of 32 up to 256, rotary pairs inside one
+// 32-row tile (GPT-J pairs; GPT-NeoX rotate-half with n_rot <= 32), n_embd <= 8192.
+bool fast_decode_ok(const vsim_model *m) {
+  const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H;
+  const int nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
+  return d % 32 == 0 && d <= 256 && E <= 8192 && E % 128 == 0 &&
+         (m->arch == VSIM_ARCH_GPTJ || m->hp.n_rot <= 32) && 2 * H * nch <= 4096;
+}
+
+int enqueue_decode_fast(vsim_model *m, int &nk) {
+  const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
+  const bool gptj = m->arch == VSIM_ARCH_GPTJ;
+  hipStream_t s = m->stream;
+  DevTables tab;
+  RC(tables_get(&tab));
+  const int nbE = E / QK, nbF = F / QK;
+  uint8_t *q1 = m->xq1, *q2 = m->xq2, *q3 = m->xq3;
+  float *d1 = (float *)(q1 + (size_t)nbE * 16), *d2 = (float *)(q2 + (size_t)nbE * 16);
+  float *d3 = (float *)(q3 + (size_t)nbF * 16);
+  if (m->first) {
+    RC(launch_get_rows(m->wte, E, V, m->tok_dev, 1, m->inpL, s));
+    ++nk;
+  }
+  const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  const int nchunk = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
+  float *R[2] = {m->inpL, m->inpL2};
+  int cur = 0;
+  for (int il = m->l0; il < m->l1; ++il) {
+    const LayerW &L = m->layers[il - m->l0];
+    const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
+    // LayerNorm(s) -> Q4 activations (GPT-J: one LayerNorm feeds attention and MLP)
+    FastLn N{};
+    N.x = R[cur];
+    N.E = E;
+    N.n = gptj ? 1 : 2;
+    N.w[0] = L.ln1_w;
+    N.b[0] = L.ln1_b;
+    N.w[1] = L.ln2_w;
+    N.b[1] = L.ln2_b;
+    N.qs[0] = q1;
+    N.d[0] = d1;
+    N.qs[1] = q2;
+    N.d[1] = d2;
+    RC(launch_fast_ln(N, s));
+    ++nk;
+    // {fc_in -> GELU -> quantize, Q, K, V}
+    FastGemv P{};
+    P.xq[0] = q1;
+    P.xd[0] = d1;
+    P.xq[1] = gptj ? q1 : q2;
+    P.xd[1] = gptj ? d1 : d2;
+    P.nj = 4;
+    P.j[0] = FastJob{w4_view(L.wfc, F, E), L.bfc, nullptr, FE_GELU_Q, 1};
+    P.j[1] = FastJob{w4_view(L.wq, E, E), gptj ? nullptr : L.bq, m->Qb, FE_ROPE_Q, 0};
+    P.j[2] = FastJob{w4_view(L.wk, E, E), gptj ? nullptr : L.bk, m->kcache + loff, FE_ROPE_K, 0};
+    P.j[3] = FastJob{w4_view(L.wv, E, E), gptj ? nullptr : L.bv, m->vcache + loff, FE_V, 0};
+    P.gelu_tab = tab.gelu_f16;
+    P.oq_qs = q3;
+    P.oq_d = d3;
+    P.npast = m->npast_dev;
+    P.cs = m->rope_cs;
+    P.d = d;
+    P.n_rot = m->hp.n_rot;
+    P.style = gptj ? 1 : 0;
+    hipEvent_t *ev = prof_begin(m);
+    RC(launch_fast_gemv(P, E, s));
+    prof_end(m, ev, w4_algo_bytes(P.j[0].w) + 3 * w4_algo_bytes(P.j[1].w));
+    ++nk;
+    // fc_out split over K | attention chunks
+    FastTail T{};
+    T.wf = w4_view(L.wproj, E, F);
+    T.xf_qs = q3;
+    T.xf_d = d3;
+    T.ffp = m->fast_ffp;
+    T.sf = FD_SF;
+    T.q = m->Qb;
+    T.kc = m->kcache + loff;
+    T.vc = m->vcache + loff;
+    T.npast = m->npast_dev;
+    T.d = d;
+    T.H = H;
+    T.nchunk = nchunk;
+    T.scale = scale;
+    T.part = m->fast_part;
+    ev = prof_begin(m);
+    RC(launch_fast_tail(T, s));
+    prof_end(m, ev, w4_algo_bytes(T.wf));
+    ++nk;
+    // attention merge + out-projection + residual join into the other buffer
+    FastOproj O{};
+    O.w = w4_view(L.wo, E, E);
+    O.part = m->fast_part;
+    O.d = d;
+    O.nchunk = nchunk;
+    O.bo = gptj ? nullptr : L.bo;
+    O.ffp = m->fast_ffp;
+    O.sf = FD_SF;
+    O.bproj = L.bproj;
+    O.x = R[cur];
+    O.out = R[cur ^ 1];
+    ev = prof_begin(m);
+    RC(launch_fast_oproj_join(O, s));
+    prof_end(m, ev, w4_algo_bytes(O.w));
+    ++nk;
+    cur ^= 1;
+  }
+  if (m->last) {
+    FastLn N{};
+    N.x = R[cur];
+    N.E = E;
+    N.n = 1;
+    N.w[0] = m->lnf_w;
+    N.b[0] = m->lnf_b;
+    N.qs[0] = q1;
+    N.d[0] = d1;
+    RC(launch_fast_ln(N, s));
+    ++nk;
+    FastGemv P{};
+    P.xq[0] = P.xq[1] = q1;
+    P.xd[0] = P.xd[1] = d1;
+    P.nj = 1;
+    P.j[0] = FastJob{w4_view(m->lmh, V, E), gptj ? m->lmh_b : nullptr, m->logits, FE_STORE, 0};
+    hipEvent_t *ev = prof_begin(m);
+    RC(launch_fast_gemv(P, E, s));
+    prof_end(m, ev, w4_algo_bytes(P.j[0].w));
+    ++nk;
+  }
+  m->resid_final = R[cur];
+  return VSIM_OK;
+}
+
 // The single-token decode step as 4 fused launches per layer (layer.hip).  Reads the token
 // from tok_dev and n_past from npast_dev, so the enqueued sequence is replayable.
 int enqueue_decode(vsim_model *m, int &nk) {
+  static const bool fast_env = [] {  // VSIM_FAST_DECODE=0: fast mode on the older kernels
+    const char *e = getenv("VSIM_FAST_DECODE");
+    return !(e && e[0] == '0');
+  }();
+  if (m->mode == VSIM_MODE_FAST && fast_env && fast_decode_ok(m)) return enqueue_decode_fast(m, nk);
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
   const bool gptj = m->arch == VSIM_ARCH_GPTJ;
   hipStream_t s = m->stream;
@@ -685,7 +837,9 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   plan_slots(m, plan);
   size_t tot = 0;
   for (auto &ps : plan) tot += (slot_dev_bytes(ps.second) + 255) & ~(size_t)255;
-  if (hipMalloc((void **)&m->warena, tot) != hipSuccess) { set_error("model_create: weight alloc failed"); return fail(VSIM_ENOMEM); }
+  // + FD_PAD: the fast GEMV streams whole 16-block batches and zeroes the scales of slots past
+  // a wave's range, so it may read up to 8 KB past a tensor (fast_decode.hip TileStream)
+  if (hipMalloc((void **)&m->warena, tot + FD_PAD) != hipSuccess) { set_error("model_create: weight alloc failed"); return fail(VSIM_ENOMEM); }
   m->wbytes = tot;
   size_t off = 0;
   for (auto &ps : plan) {
