@@ -92,3 +92,24 @@ def test_fast_decode_deterministic(tmp_path, name):
     a = m.eval(len(ids), [tok]).copy()
     b = m.eval(len(ids), [tok]).copy()
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("dims", [
+    # GPT-J-6B and pythia-12b widths, 2 layers: multi-batch weight streams per wave, K splits
+    # of fc_out beyond one LDS slice, d = 256 / 128 heads, rotary pairs of both styles
+    (hip.ARCH_GPTJ, dict(n_vocab=4096, n_embd=4096, n_head=16, n_layer=2, n_rot=64, use_parallel_residual=1)),
+    (hip.ARCH_GPTNEOX, dict(n_vocab=4096, n_embd=5120, n_head=40, n_layer=2, n_rot=32, use_parallel_residual=1)),
+])
+def test_fast_decode_full_width(dims):
+    """At full width (4096-20480 activations re-quantized per layer) some 4-bit quantum flips
+    in nearly every step (measured cos ~0.992, max-rel ~0.12 at 2 layers); a kernel error
+    (e.g. a wrong LDS slot) shows up as cos << 0.9 or NaN."""
+    arch, hp = dims
+    m = hip.Model.create(arch, hp, n_ctx=605)
+    m.randomize(seed=3, std=0.02)
+    m.set_mode(hip.MODE_EXACT)
+    tok = int(np.argmax(m.eval(0, [50, 60, 70, 80, 90])))
+    res = _teacher_forced(m, 5, tok, 6)
+    print([(round(c, 5), round(r, 6), a) for c, r, a in res])
+    assert all(c > 0.98 for c, _, _ in res), res
+    assert sum(a for _, _, a in res) >= 4, res

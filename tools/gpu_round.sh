@@ -1,0 +1,32 @@
+#!/bin/bash
+# tools/gpu_round.sh TAG — the round's measurement pass on one GPU box: the default bench line
+# (exact value + fast companion + CPU baseline), rocprofv3 kernel summaries of exact decode,
+# fast decode and the codegen-16B prefill, and FETCH_SIZE passes (HBM traffic) of both decode
+# modes.  Every GPU step has its own time limit; a fatal exit ends the script.
+set -u
+tag=${1:-r01}
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/gpurun_out
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+fatal() { local rc=$1; echo "[gpu_round] $2 exit=$rc"; if [ "$rc" -ne 0 ]; then exit "$rc"; fi; }
+timeout -k 10 400 python3 "$root/bench.py" > "$out/bench_default_$tag.log" 2>&1
+fatal $? bench; tail -1 "$out/bench_default_$tag.log"
+timeout -k 10 300 python3 "$root/bench.py" --config codegen-16B --prefill 2048 --steps 3 > "$out/bench_prefill_$tag.log" 2>&1
+fatal $? prefill; tail -1 "$out/bench_prefill_$tag.log"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_exact_$tag" -o run --output-format csv -- \
+  python3 "$root/bench.py" --steps 64 --warmup 4 --no-cpu-baseline --no-fast --no-profile > "$out/prof_exact_$tag.log" 2>&1
+fatal $? prof_exact
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_fast_$tag" -o run --output-format csv -- \
+  python3 "$root/bench.py" --mode fast --steps 64 --warmup 4 --no-cpu-baseline --no-profile > "$out/prof_fast_$tag.log" 2>&1
+fatal $? prof_fast
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_prefill_$tag" -o run --output-format csv -- \
+  python3 "$root/bench.py" --config codegen-16B --prefill 2048 --steps 2 > "$out/prof_prefill_$tag.log" 2>&1
+fatal $? prof_prefill
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_exact_$tag" -o run --output-format csv -- \
+  python3 "$root/bench.py" --steps 8 --warmup 2 --no-cpu-baseline --no-profile --no-fast > "$out/pmc_exact_$tag.log" 2>&1
+fatal $? pmc_exact
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fast_$tag" -o run --output-format csv -- \
+  python3 "$root/bench.py" --mode fast --steps 8 --warmup 2 --no-cpu-baseline --no-profile > "$out/pmc_fast_$tag.log" 2>&1
+fatal $? pmc_fast
+echo "[gpu_round] done"

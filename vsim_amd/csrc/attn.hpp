@@ -10,20 +10,29 @@
 
 namespace vsim {
 
-// One workgroup per head.  KQ: one wave per key, products over the head
-// dimension summed as a tree in double; the reference's sequential double sum lies within
-// 2*d*2^-53*sum|p| of it, so when both ends of that interval round to the same float the
-// score is the reference's, otherwise lane 0 redoes the key sequentially (ggml.c:4760-4800
-// for the f32 dot with a double accumulator).  KQV keeps the reference's sequential float
-// chain over the keys, one chain per output element.
-constexpr int ATT_KB = 4;   // keys per wave per load group
-constexpr int ATT_DPL = 4;  // max head-dim elements per lane (d <= 256)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// One head (h) per workgroup of NT threads; sm: (2d + n_past + 1) floats of LDS.
+// One workgroup per head.  KQ: 16 lanes per key (four keys per wave instruction, KB
+// steps loaded at once), products over the head dimension summed as a tree in double; the
+// reference's sequential double sum lies within 2*d*2^-53*sum|p| of it, so when both ends of
+// that interval round to the same float the score is the reference's, otherwise the key is
+// redone sequentially by one lane (ggml.c:4760-4800 for the f32 dot with a double
+// accumulator).  KQV keeps the reference's sequential float chain over the keys, one chain
+// per output element; the V rows stream through LDS tiles, three tiles in flight.
+constexpr int ATT_KB = 4;       // KQ: four-key steps per wave per load batch
+constexpr int ATT_DPL = 4;      // max float4 of the head dimension per lane in KQ (d <= 256)
+
+// One head (h) per workgroup of NT >= d threads; sm: attn_lds_floats(d, n_ctx) floats of LDS.
+// prof (timing experiments only): s_memtime stamps of head 0's phases, thread 0
+// Work item hs = head * S + part, S = A.nsplit (>= 1): every part computes the head's scores
+// and softmax (identical in each), then the KQV chains and quantization of output columns
+// [part*c, part*c + c), c = d / S, so a head's V rows spread over S CUs.  Every part writes
+// the same new K/V cache row (identical bytes) before reading it back.
 template <int NT>
-__device__ __forceinline__ void attn_body(const AttnJob &A, int h, float *sm) {
+__device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, unsigned long long *prof = nullptr) {
   constexpr int ATT_THREADS = NT, ATT_WAVES = NT / 64;
-  const int d = A.d, E = A.d * A.H;
+  const int S = A.nsplit > 1 ? A.nsplit : 1, h = hs / S, part = hs % S;
+  const int d = A.d, E = A.d * A.H, c = d / S, c0 = part * c;
   const int n_past = *A.npast;
   const int nk = n_past + 1;
   float *qh = sm;           // [d]
@@ -32,6 +41,8 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int h, float *sm) {
   __shared__ float shf[ATT_WAVES];
   __shared__ double shd[ATT_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  prof = part == 0 ? prof : nullptr;
+  if (prof && h == 0 && tid == 0) prof[0] = __builtin_amdgcn_s_memtime();
   for (int i = tid; i < d; i += ATT_THREADS) {
     qh[i] = A.q[h * d + i];
     kh[i] = A.k[h * d + i];
@@ -58,53 +69,72 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int h, float *sm) {
   }
   __syncthreads();
   for (int i = tid; i < d; i += ATT_THREADS) A.kc[(size_t)n_past * E + h * d + i] = kh[i];
+  if (prof && h == 0 && tid == 0) prof[1] = __builtin_amdgcn_s_memtime();
   // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale.
-  // Each wave takes keys in groups of ATT_KB and loads the whole group before reducing, so
-  // the cache reads of a group overlap (one wave per key would pay the latency per key).
+  // Row r (lanes 16r..16r+15) of a wave takes one key per step; lane l16 covers the float4s
+  // at 4*l16 + 64*e of the head dimension.  A wave loads ATT_KB steps (4*ATT_KB keys) at once.
   float mx = -INFINITY;
-  for (int k0 = wid * ATT_KB; k0 < nk; k0 += ATT_WAVES * ATT_KB) {
-    float kv[ATT_KB][ATT_DPL];
+  {
+    const int row = lane >> 4, l16 = lane & 15;
+    float4 q4[ATT_DPL];
 #pragma unroll
-    for (int j = 0; j < ATT_KB; ++j) {
-      const int k = min(k0 + j, nk - 1);
-      const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
-#pragma unroll
-      for (int e = 0; e < ATT_DPL; ++e) {
-        const int i = lane + 64 * e;
-        kv[j][e] = i < d ? kr[i] : 0.0f;
-      }
+    for (int e = 0; e < ATT_DPL; ++e) {
+      const int i = 4 * l16 + 64 * e;
+      q4[e] = i < d ? *(const float4 *)(qh + i) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    for (int k0 = wid * 4 * ATT_KB; k0 < nk; k0 += ATT_WAVES * 4 * ATT_KB) {
+      float4 kv[ATT_KB][ATT_DPL];
 #pragma unroll
-    for (int j = 0; j < ATT_KB; ++j) {
-      const int k = k0 + j;
-      if (k >= nk) break;  // wave-uniform
-      double t = 0.0, ta = 0.0;
+      for (int j = 0; j < ATT_KB; ++j) {
+        const int k = min(k0 + 4 * j + row, nk - 1);
+        const float *kr = A.kc + (size_t)k * E + h * d;
 #pragma unroll
-      for (int e = 0; e < ATT_DPL; ++e) {
-        const int i = lane + 64 * e;
-        if (i < d) {
-          const double p = (double)(kv[j][e] * qh[i]);
-          t += p;
-          ta += fabs(p);
+        for (int e = 0; e < ATT_DPL; ++e) {
+          const int i = 4 * l16 + 64 * e;
+          kv[j][e] = i < d ? *(const float4 *)(kr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      t = wave_sum_d(t);
-      ta = wave_sum_d(ta);
-      const double bnd = 2.0 * d * 0x1.0p-53 * ta;
-      float sc = (float)(t - bnd);
-      if (sc != (float)(t + bnd)) {  // wave-uniform: redo this key in the reference order
-        const float *kr = k == n_past ? kh : A.kc + (size_t)k * E + h * d;
-        double acc = 0.0;
-        if (lane == 0)
-          for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
-        sc = (float)__shfl(acc, 0, 64);
+#pragma unroll
+      for (int j = 0; j < ATT_KB; ++j) {
+        const int k = k0 + 4 * j + row;
+        double t = 0.0, ta = 0.0;
+#pragma unroll
+        for (int e = 0; e < ATT_DPL; ++e) {
+          const double p0 = (double)(kv[j][e].x * q4[e].x), p1 = (double)(kv[j][e].y * q4[e].y);
+          const double p2 = (double)(kv[j][e].z * q4[e].z), p3 = (double)(kv[j][e].w * q4[e].w);
+          t += (p0 + p1) + (p2 + p3);
+          ta += (fabs(p0) + fabs(p1)) + (fabs(p2) + fabs(p3));
+        }
+        // sum over the row's 16 lanes (every lane of the row ends with the total)
+        auto add = [](double a, double b) { return a + b; };
+        t = add(t, dpp::mov<dpp::QP_XOR1, 0xF>(t, 0.0));
+        ta = add(ta, dpp::mov<dpp::QP_XOR1, 0xF>(ta, 0.0));
+        t = add(t, dpp::mov<dpp::QP_XOR2, 0xF>(t, 0.0));
+        ta = add(ta, dpp::mov<dpp::QP_XOR2, 0xF>(ta, 0.0));
+        t = add(t, dpp::mov<dpp::HALF_MIRROR, 0xF>(t, 0.0));
+        ta = add(ta, dpp::mov<dpp::HALF_MIRROR, 0xF>(ta, 0.0));
+        t = add(t, dpp::mov<dpp::MIRROR, 0xF>(t, 0.0));
+        ta = add(ta, dpp::mov<dpp::MIRROR, 0xF>(ta, 0.0));
+        const double bnd = 2.0 * d * 0x1.0p-53 * ta;
+        float sc = (float)(t - bnd);
+        if (k < nk && sc != (float)(t + bnd)) {  // row-uniform: redo this key in the reference order
+          if (l16 == 0) {
+            const float *kr = A.kc + (size_t)k * E + h * d;
+            double acc = 0.0;
+            for (int i = 0; i < d; ++i) acc += (double)(kr[i] * qh[i]);
+            sc = (float)acc;
+          }
+        }
+        sc = sc * A.scale;
+        if (k < nk) {
+          if (l16 == 0) pr[k] = sc;
+          mx = mx > sc ? mx : sc;
+        }
       }
-      sc = sc * A.scale;
-      if (lane == 0) pr[k] = sc;
-      mx = mx > sc ? mx : sc;
     }
   }
   // max, exp via table, exact double sum (fp16 values: any order), 1/sum
+  if (prof && h == 0 && tid == 0) prof[2] = __builtin_amdgcn_s_memtime();
   mx = wave_max_f(mx);
   if (lane == 0) shf[wid] = mx;
   __syncthreads();
@@ -124,31 +154,70 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int h, float *sm) {
   const float inv = (float)(1.0 / sum);
   for (int k = tid; k < nk; k += ATT_THREADS) pr[k] = pr[k] * inv;
   __syncthreads();
-  // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f; V rows loaded
-  // 16 keys ahead of the chain
-  for (int dd0 = 0; dd0 < d; dd0 += ATT_THREADS) {
-    const int dd = dd0 + tid;
-    float y = 0.0f;
-    if (dd < d) {
-      const float *vcol = A.vc + h * d + dd;
-      int k = 0;
-      for (; k + 16 <= nk; k += 16) {
-        float vv[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) vv[j] = vcol[(size_t)(k + j) * E];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) y = y + vv[j] * pr[k + j];
-      }
-      for (; k < nk; ++k) y = y + vcol[(size_t)k * E] * pr[k];
-      if (A.out) A.out[h * d + dd] = y;
-    }
-    // quantize the head's outputs, two 32-blocks per wave
-    if (dd0 + wid * 64 < d) {
-      const int blk = (h * d + dd0 + wid * 64) / QK + (lane >> 5);
-      const bool ok = dd0 + wid * 64 + (lane & ~31) < d;
-      quantize_half(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
-    }
+  if (prof && h == 0 && tid == 0) prof[3] = __builtin_amdgcn_s_memtime();
+  // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f (product and sum
+  // rounded separately), thread j < c for column dd = c0 + j.  Every thread loads V tiles
+  // (KT keys x c floats, float4 per slot) three tiles ahead into registers and stores them
+  // into two LDS buffers; the chains read the tile from LDS.  (The KV-cache row n_past,
+  // written above by this workgroup, is read back after the barriers.)
+  float y = 0.0f;  // (c <= ATT_THREADS: one output element per thread)
+  {
+    constexpr int PER = (ATT_VTF / 4 + ATT_THREADS - 1) / ATT_THREADS;  // float4 per thread per tile
+    const int KT = ATT_VTF / c, nt = (nk + KT - 1) / KT, n4 = KT * c / 4;
+    float *const vt0 = sm + ((2 * d + A.n_ctx + 3) & ~3);  // buffer b at vt0 + b * ATT_VTF
+// (macros, not lambdas: the register ring must not be passed by address, or the compiler
+// keeps it in scratch and waits for every load)
+#define ATT_TLOAD(R, T)                                                              \
+  _Pragma("unroll") for (int q = 0; q < PER; ++q) {                                  \
+    const int f = min(tid + ATT_THREADS * q, n4 - 1);                                \
+    const int key = min((T) * KT + (4 * f) / c, nk - 1), col = c0 + (4 * f) % c;     \
+    R[q] = *(const f32x4 *)(A.vc + (size_t)key * E + h * d + col);                   \
   }
+    f32x4 ra[PER], rb[PER], rc[PER];  // tiles t, t+1, t+2 in flight (clang vectors: HIP's
+                                      // float4 class arrays are not promoted to registers)
+    ATT_TLOAD(ra, 0)
+    if (nt > 1) { ATT_TLOAD(rb, 1) }
+    if (nt > 2) { ATT_TLOAD(rc, 2) }
+    for (int t = 0; t < nt; ++t) {
+      float *buf = vt0 + (t & 1) * ATT_VTF;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int f = tid + ATT_THREADS * q;
+        if (f < n4) *(f32x4 *)(buf + 4 * f) = ra[q];
+        ra[q] = rb[q];
+        rb[q] = rc[q];
+      }
+      __syncthreads();
+      if (t + 3 < nt) { ATT_TLOAD(rc, t + 3) }
+      if (tid < c) {  // the chain: LDS reads eight keys ahead of the dependent adds
+        const int kn = min(KT, nk - t * KT);
+        const float *pt = pr + t * KT;
+        int j = 0;
+        for (; j + 8 <= kn; j += 8) {
+          float v[8], p[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            v[u] = buf[(j + u) * c + tid];
+            p[u] = pt[j + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) y = y + v[u] * p[u];
+        }
+        for (; j < kn; ++j) y = y + buf[j * c + tid] * pt[j];
+      }
+    }
+#define ATT_STEP
+#undef ATT_STEP
+#undef ATT_TLOAD
+    if (tid < c && A.out) A.out[h * d + c0 + tid] = y;
+  }
+  // quantize the part's outputs: wave w holds columns c0 + 64w .. +63, two 32-blocks
+  if (wid * 64 < c) {
+    const int blk = (h * d + c0 + wid * 64) / QK + (lane >> 5);
+    const bool ok = wid * 64 + (lane & ~31) < c;
+    quantize_half(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
+  }
+  if (prof && h == 0 && tid == 0) prof[4] = __builtin_amdgcn_s_memtime();
 }
 
 }  // namespace vsim

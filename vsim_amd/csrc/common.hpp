@@ -93,11 +93,19 @@ struct AttnJob {
   const double2 *cs;       // RoPE cos/sin table [n_ctx][n_rot/2]
   const uint16_t *etab;    // table_exp_f16
   int d, H, n_rot, style;  // style 0 = GPT-NeoX rotate-half, 1 = GPT-J pairs
+  int n_ctx;               // cache rows (sizes the LDS score array, attn_lds_floats)
+  int nsplit;              // workgroups per head (column parts of KQV, attn.hpp); 0/1 = one
   float scale;
   uint8_t *oq_qs;          // output activation, Q4 SoA (E/32 blocks)
   float *oq_d, *oxd;
   float *out;              // optional float copy [E]
 };
+
+// exact decode attention (attn.hpp): LDS floats for q, k, the scores and two V tiles
+constexpr int ATT_VTF = 8192;  // floats per V tile (32 KB)
+__host__ __device__ constexpr int attn_lds_floats(int d, int n_ctx) {
+  return ((2 * d + n_ctx + 3) & ~3) + 2 * ATT_VTF;
+}
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s);
 // out[i] = x[i] + ((a[i] + ab[i]) + (f[i] + fb[i]))  (ab may be null): the residual join alone

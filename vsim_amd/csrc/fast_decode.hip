@@ -105,6 +105,7 @@ struct TileStream {
   const uint8_t *qs;  // tile's nibble plane: block b row r at (b*32 + r)*16
   const float *dd;    // tile's scale plane: (b*32 + r)
   int b0, b1, lane;
+  int xoff = 0;  // first block of the activation slice staged in LDS
   uint4 qa[FD_U];
   float da[FD_U];
 
@@ -129,7 +130,7 @@ struct TileStream {
 #pragma unroll
     for (int u = 0; u < FD_U; ++u) {
       const int bu = b0 + h + 2 * (it * FD_U + u);
-      const int b = min(bu, b1 - 1);
+      const int b = min(bu, b1 - 1) - xoff;  // activation slot in LDS
       const uint4 x = xq[b];
       int s = __builtin_amdgcn_sdot8((int)(q[u].x ^ 0x88888888u), (int)x.x, 0, false);
       s = __builtin_amdgcn_sdot8((int)(q[u].y ^ 0x88888888u), (int)x.y, s, false);
@@ -181,7 +182,9 @@ struct ActStage {
   uint4 v;
   float d;
   int b;
-  __device__ __forceinline__ void load(const uint8_t *qs, const float *dp, int b0, int b1) {
+  int b0;
+  __device__ __forceinline__ void load(const uint8_t *qs, const float *dp, int b0_, int b1) {
+    b0 = b0_;
     b = b0 + (int)threadIdx.x;
     if (b < b1) {
       v = *(const uint4 *)(qs + (size_t)b * 16);
@@ -189,9 +192,9 @@ struct ActStage {
     }
   }
   __device__ __forceinline__ void store(int b1, uint4 *xq, float *xd) const {
-    if (b < b1) {
-      xq[b] = make_uint4(v.x ^ 0x88888888u, v.y ^ 0x88888888u, v.z ^ 0x88888888u, v.w ^ 0x88888888u);
-      xd[b] = d;
+    if (b < b1) {  // LDS slot b - b0
+      xq[b - b0] = make_uint4(v.x ^ 0x88888888u, v.y ^ 0x88888888u, v.z ^ 0x88888888u, v.w ^ 0x88888888u);
+      xd[b - b0] = d;
     }
   }
 };
@@ -431,6 +434,7 @@ __global__ void __launch_bounds__(FT_NT, 6) k_fast_tail(FastTail A) {
   ts.b0 = kb0 + wave * (kb1 - kb0) / FD_WAVES;
   ts.b1 = kb0 + (wave + 1) * (kb1 - kb0) / FD_WAVES;
   ts.lane = lane;
+  ts.xoff = kb0;
   ActStage st;
   st.load(A.xf_qs, A.xf_d, kb0, kb1);
   ts.prefetch();

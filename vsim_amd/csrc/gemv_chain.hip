@@ -674,16 +674,17 @@ __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
     return;
   }
   b -= T.nf;
-  if (b < T.a.H) {
+  const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
+  if (b < na) {
     attn_body<C2_THREADS>(T.a, b, L.a);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's output stores
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  b -= T.a.H;
+  b -= na;
   if (threadIdx.x == 0)
-    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)T.a.H)
+    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)na)
       __builtin_amdgcn_s_sleep(8);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -692,7 +693,9 @@ __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
 
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
                       hipStream_t s) {
-  if (a.d % 32 != 0 || a.d > 64 * ATT_DPL || (size_t)(2 * a.d + n_ctx) * sizeof(float) > sizeof(C2Lds)) {
+  const int S = a.nsplit > 1 ? a.nsplit : 1;
+  if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
+      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds)) {
     set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
     return VSIM_EINVAL;
   }
@@ -707,7 +710,7 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;
   // dynamic LDS pad: above half the CU's LDS, so one workgroup per CU (fc_out's consumer
   // keeps its SIMD); the out-projection tiles that find no CU start as attention heads end
-  hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H + no), dim3(C2_THREADS), 8192, s, T);
+  hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H * S + no), dim3(C2_THREADS), 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

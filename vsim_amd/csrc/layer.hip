@@ -147,23 +147,32 @@ int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s) {
 // ------------------------------------------------------------------ 3. attention (N = 1)
 // attn.hpp; one 1024-thread workgroup per head
 constexpr int ATT_THREADS = 1024;
+__device__ unsigned long long g_attn_prof[8];  // timing experiment output (VSIM_ATT_DBG)
+template <bool PROF>
 __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  attn_body<ATT_THREADS>(A, blockIdx.x, sm);
+  attn_body<ATT_THREADS>(A, blockIdx.x, sm, PROF ? g_attn_prof : nullptr);
 }
 
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s) {
-  if (A.d % 32 != 0 || A.d > 64 * ATT_DPL) {
+  const int S = A.nsplit > 1 ? A.nsplit : 1;
+  if (A.d % 32 != 0 || A.d > 256 || A.n_ctx != n_ctx || A.d % S != 0 || (A.d / S) % QK != 0) {
     set_error("attention: head dim must be a multiple of 32, at most 256");
     return VSIM_EINVAL;
   }
-  const size_t smem = (size_t)(2 * A.d + n_ctx) * sizeof(float);
-  hipLaunchKernelGGL(k_attn_decode, dim3(A.H), dim3(ATT_THREADS), smem, s, A);
+  const size_t smem = (size_t)attn_lds_floats(A.d, n_ctx) * sizeof(float);
+  static const bool prof = getenv("VSIM_ATT_DBG") != nullptr;
+  if (prof) hipLaunchKernelGGL(k_attn_decode<true>, dim3(A.H * S), dim3(ATT_THREADS), smem, s, A);
+  else hipLaunchKernelGGL(k_attn_decode<false>, dim3(A.H * S), dim3(ATT_THREADS), smem, s, A);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
 
 }  // namespace vsim
+
+extern "C" int vsim_debug_attn_prof(unsigned long long *out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(vsim::g_attn_prof), sizeof(vsim::g_attn_prof)) == hipSuccess ? 0 : -1;
+}
 
 extern "C" int vsim_debug_ln_prof(unsigned long long *out8) {
   return hipMemcpyFromSymbol(out8, HIP_SYMBOL(vsim::g_ln_prof), sizeof(vsim::g_ln_prof)) == hipSuccess ? 0 : -1;

@@ -634,7 +634,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       join_into(j2, false);
     }
     const bool tail = tail_env && !split && m->mode == VSIM_MODE_EXACT &&
-                      (size_t)(2 * d + m->n_ctx) * sizeof(float) <= 75264;
+                      (size_t)attn_lds_floats(d, m->n_ctx) * sizeof(float) <= 75264;
     if (tail) j1.clear = m->tail_done;
     RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
     ++nk;
@@ -698,6 +698,17 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.H = H;
     A.n_rot = m->hp.n_rot;
     A.style = gptj ? 1 : 0;
+    A.n_ctx = m->n_ctx;
+    // column parts per head (attn.hpp); VSIM_ATT_SPLIT overrides (A/B timing)
+    {
+      static const int split_env = [] {
+        const char *e = getenv("VSIM_ATT_SPLIT");
+        return e ? atoi(e) : 0;
+      }();
+      int S = split_env > 0 ? split_env : 1;
+      while (S > 1 && (d % S != 0 || (d / S) % QK != 0)) --S;
+      A.nsplit = S;
+    }
     A.scale = scale;
     A.oq_qs = qa;
     A.oq_d = da;
