@@ -10,8 +10,6 @@
 
 namespace vsim {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
 // One workgroup per head.  KQ: 16 lanes per key (four keys per wave instruction, KB
 // steps loaded at once), products over the head dimension summed as a tree in double; the
 // reference's sequential double sum lies within 2*d*2^-53*sum|p| of it, so when both ends of

@@ -22,6 +22,11 @@ constexpr int QBYTES = 20;   // fp32 d + 16 nibble bytes (ggml.c:907-909)
 // scale plane d: block (r, b) lives at index ((r/32)*nb + b)*32 + r%32 of both.
 constexpr int T32 = 32;
 
+// clang vector types for register arrays: arrays of HIP's float4/uint4 classes that are
+// copied or conditionally assigned are not promoted to registers (they land in scratch)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 struct W4 {
   const uint8_t *qs;
   const float *d;

@@ -70,6 +70,7 @@ struct FastTail {
 struct FastOproj {
   W4 w;                    // out-projection E x E
   const float *part;       // attention chunk partials (FastTail::part)
+  const int *npast;
   int d, nchunk;
   const float *bo;         // may be null (GPT-J)
   const float *ffp;        // [sf][E]

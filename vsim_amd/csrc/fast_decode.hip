@@ -100,7 +100,6 @@ __device__ __forceinline__ int dot_q4(uint4 q, uint4 x) {
 // lane & 31), FD_U loads per lane in flight, the next batch issued before the current one
 // is consumed.  The activation (nibbles + scales) is read from LDS.  `pre` tells whether
 // batch 0 was already issued by the caller (into qa/da).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct TileStream {
   const uint8_t *qs;  // tile's nibble plane: block b row r at (b*32 + r)*16
   const float *dd;    // tile's scale plane: (b*32 + r)
@@ -354,11 +353,11 @@ __device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
     return;
   }
   const int pw = p0 + wid * FD_PPW;
-  float4 kv4[FD_PPW], vv4[FD_PPW];
+  f32x4 kv4[FD_PPW], vv4[FD_PPW];  // (clang vectors: kept in registers)
 #pragma unroll
   for (int j = 0; j < FD_PPW; ++j) {
     const int p = min(pw + j, p1 - 1);
-    kv4[j] = act ? *(const float4 *)(A.kc + (size_t)p * E + h * d + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    kv4[j] = act ? *(const f32x4 *)(A.kc + (size_t)p * E + h * d + e0) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   float t[FD_PPW];
 #pragma unroll
@@ -373,7 +372,7 @@ __device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
 #pragma unroll
   for (int j = 0; j < FD_PPW; ++j) {
     const int p = min(pw + j, p1 - 1);
-    vv4[j] = act ? *(const float4 *)(A.vc + (size_t)p * E + h * d + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    vv4[j] = act ? *(const f32x4 *)(A.vc + (size_t)p * E + h * d + e0) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
   for (int j = 0; j < FD_PPW; ++j) {
@@ -452,10 +451,11 @@ __global__ void __launch_bounds__(FT_NT, 6) k_fast_tail(FastTail A) {
 // Merge over all nchunk chunks, FD_MG at a time, with every load of a group (the chunks'
 // m, l and this thread's o values) issued together; chunks past n_past weigh zero.
 constexpr int FD_MAXW = 4096;  // merge weights in LDS: heads x chunks
-constexpr int FD_MG = 4;       // chunks per load group
+constexpr int FD_MG = 8;       // chunks per load group
 template <int NT>
 __device__ __forceinline__ void attn_merge_lds(const FastOproj &P, int E, uint4 *xq, float *xd, float *wgt) {
   const int tid = threadIdx.x, d = P.d, H = E / d, nch = P.nchunk;
+  const int nv = min(*P.npast / FD_CHUNK + 1, nch);  // chunks holding positions 0 .. n_past
   // (m, l) of every (head, chunk) into LDS: wgt[h*nch + c] = m, wgt[H*nch + h*nch + c] = l
   for (int x = tid; x < H * nch; x += NT) {
     const float *pc = P.part + (size_t)x * (d + 2);
@@ -483,14 +483,14 @@ __device__ __forceinline__ void attn_merge_lds(const FastOproj &P, int E, uint4 
     const int ic = ok ? i : 0, h = ic / d;
     const float *src = P.part + (size_t)h * nch * (d + 2) + 2 + (ic - h * d);
     float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c0 = 0; c0 < nch; c0 += FD_MG) {
+    for (int c0 = 0; c0 < nv; c0 += FD_MG) {  // chunks past n_past weigh zero: skipped
       float4 o[FD_MG];
 #pragma unroll
       for (int u = 0; u < FD_MG; ++u)
-        o[u] = c0 + u < nch ? *(const float4 *)(src + (size_t)(c0 + u) * (d + 2)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        o[u] = c0 + u < nv ? *(const float4 *)(src + (size_t)(c0 + u) * (d + 2)) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int u = 0; u < FD_MG; ++u) {
-        const float w = c0 + u < nch ? wgt[h * nch + c0 + u] : 0.0f;
+        const float w = c0 + u < nv ? wgt[h * nch + c0 + u] : 0.0f;
         y.x = __builtin_fmaf(o[u].x, w, y.x);
         y.y = __builtin_fmaf(o[u].y, w, y.y);
         y.z = __builtin_fmaf(o[u].z, w, y.z);

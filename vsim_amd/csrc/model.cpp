@@ -207,7 +207,7 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMemset(m->tail_done, 0, sizeof(unsigned)));
   {
     const size_t d = E / H, nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
-    VSIM_HIP(fa(&m->fast_ffp, FD_SF * E));
+    VSIM_HIP(fa(&m->fast_ffp, 8 * E));
     VSIM_HIP(fa(&m->fast_part, H * nch * (d + 2)));
     VSIM_HIP(hipMemset(m->fast_part, 0, H * nch * (d + 2) * sizeof(float)));  // finite stale values
   }
@@ -445,6 +445,16 @@ double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 // the same replayable form as enqueue_decode (token and n_past from device memory).
 // Shapes the fast step handles: head dim a multiple of 32 up to 256, rotary pairs inside one
 // 32-row tile (GPT-J pairs; GPT-NeoX rotate-half with n_rot <= 32), n_embd <= 8192.
+// fc_out K splits: FD_SF, or VSIM_FAST_SF (1, 2, 4 or 8; A/B timing)
+int fast_sf() {
+  static const int sf = [] {
+    const char *e = getenv("VSIM_FAST_SF");
+    const int v = e ? atoi(e) : FD_SF;
+    return v == 1 || v == 2 || v == 4 || v == 8 ? v : FD_SF;
+  }();
+  return sf;
+}
+
 bool fast_decode_ok(const vsim_model *m) {
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H;
   const int nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
@@ -517,7 +527,7 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     T.xf_qs = q3;
     T.xf_d = d3;
     T.ffp = m->fast_ffp;
-    T.sf = FD_SF;
+    T.sf = fast_sf();
     T.q = m->Qb;
     T.kc = m->kcache + loff;
     T.vc = m->vcache + loff;
@@ -535,11 +545,12 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     FastOproj O{};
     O.w = w4_view(L.wo, E, E);
     O.part = m->fast_part;
+    O.npast = m->npast_dev;
     O.d = d;
     O.nchunk = nchunk;
     O.bo = gptj ? nullptr : L.bo;
     O.ffp = m->fast_ffp;
-    O.sf = FD_SF;
+    O.sf = fast_sf();
     O.bproj = L.bproj;
     O.x = R[cur];
     O.out = R[cur ^ 1];
