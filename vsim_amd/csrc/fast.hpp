@@ -12,7 +12,7 @@ constexpr int FD_OWAVES = 16;        // waves per K3 workgroup (only E/32 tiles)
 constexpr int FD_U = 4;              // 16-byte weight loads in flight per lane and batch
 constexpr int FD_MAXE = 8192;        // largest n_embd / activation length handled
 constexpr int FD_CHUNK = 64;         // attention positions per chunk workgroup
-constexpr int FD_SF = 4;
+constexpr int FD_SF = 2;
 constexpr size_t FD_PAD = 64 << 10;  // readable slack after the weight arena (TileStream)             // fc_out K splits (partial rows summed by K3)
 // GEMV epilogues: store (+bias); fc_in bias + GELU + quantize; Q with RoPE; K with RoPE
 // into the KV cache at n_past; V into the cache at n_past
