@@ -44,24 +44,28 @@ GEMV_KERNELS = ("k_gemv_chain", "k_gemv_solo", "k_layer_tail", "k_gemv_fast")
 # bench (tools/profile_round.sh) committed under profiles/; FETCH_SIZE is in KiB and reads
 # half of the bytes of a 16-byte-per-lane streaming read on gfx950 (MI355X_MICROARCH.md,
 # HBM section), so it is doubled.
-def pmc_file():
-    """The newest profiles/rNN_pmc_fetch_exact.csv (tools/profile_round.sh), or None."""
+def pmc_file(mode="exact"):
+    """The newest profiles/rNN_pmc_fetch_<mode>.csv (tools/gpu_round.sh), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch_exact.csv")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_fetch_{mode}.csv")))
     return files[-1] if files else None
 
 
-def pmc_traffic_per_launch(path=None):
+FAST_KERNELS = ("k_fast_gemv", "k_fast_tail", "k_fast_oproj_join")
+
+
+def pmc_traffic_per_launch(path=None, mode="exact"):
     """Mean corrected FETCH_SIZE bytes per GEMV launch, or None when no PMC pass is committed."""
     import csv
-    path = path or pmc_file()
+    path = path or pmc_file(mode)
     if not path or not os.path.exists(path):
         return None
+    names = GEMV_KERNELS if mode == "exact" else FAST_KERNELS
     vals = []
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name", "")
-            if r.get("Counter_Name") == "FETCH_SIZE" and any(k in name for k in GEMV_KERNELS):
+            if r.get("Counter_Name") == "FETCH_SIZE" and any(k in name for k in names):
                 vals.append(float(r["Counter_Value"]) * 1024.0 * 2.0)
     return sum(vals) / len(vals) if vals else None
 
@@ -137,6 +141,8 @@ def fast_companion(model, n_past, tok, steps):
     return {"value": round(steps / dt, 3), "unit": "tokens/s", "steps": steps,
             "weight_stream_GBps": round(gbs, 1), "frac_of_peak": round(gbs / PEAK_HBM_GBS, 4),
             "kernels": "k_fast_ln, k_fast_gemv, k_fast_tail, k_fast_oproj_join (fast_decode.hip)",
+            "traffic_per_gemv_launch": (round(pmc_traffic_per_launch(mode="fast"))
+                                        if pmc_traffic_per_launch(mode="fast") else None),
             "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": agree / len(rel),
             "parity": "not bit-exact; drifts across steps (tools/mode_drift.py)"}
 
@@ -369,11 +375,12 @@ def main():
             avg_ms = prof["gemv_ms"] / prof["gemv_launches"]
             bytes_per_launch = prof["gemv_bytes"] / prof["gemv_launches"]
             achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-            traffic = pmc_traffic_per_launch() if args.mode == "exact" and args.config == "gpt-j-6B" else None
+            traffic = pmc_traffic_per_launch(mode=args.mode) if args.config == "gpt-j-6B" else None
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4),
                         "traffic": round(traffic) if traffic else None,
-                        "kernel": "k_gemv_solo/k_layer_tail/k_gemv_chain32" if args.mode == "exact" else "k_gemv_fast*",
+                        "kernel": "k_gemv_solo/k_layer_tail/k_gemv_chain32" if args.mode == "exact"
+                        else "k_fast_gemv/k_fast_tail/k_fast_oproj_join",
                         "bytes_per_launch": round(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 3),
                         "launches": prof["gemv_launches"],
                         "gemv_share_of_step": round(prof["gemv_ms"] / 1e3 / prof_wall, 4),
