@@ -54,6 +54,8 @@ extern "C" {
 /* architectures */
 #define VSIM_ARCH_GPTNEOX 0 /* vsim.cpp:470-747                                      */
 #define VSIM_ARCH_GPTJ 1    /* ggml GPT-J graph composed from the same ops           */
+#define VSIM_ARCH_BLOOM 2   /* BLOOM graph (ALiBi, fused QKV) composed from the same ops
+                               + ggml_alibi (ggml.c:6184-6244); convert_bloom_to_ggml.py */
 
 const char *vsim_last_error(void);
 int vsim_device_count(void);

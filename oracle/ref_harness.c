@@ -87,6 +87,17 @@ int main(int argc, char **argv) {
     struct ggml_tensor *y = ggml_soft_max(ctx, ggml_diag_mask_inf(ctx, ggml_scale(ctx, x, ggml_new_f32(ctx, sc)), n_past));
     run(ctx, y);
     spit(argv[8], y->data, ggml_nbytes(y));
+  } else if (!strcmp(op, "attnsm_alibi")) {
+    /* attnsm_alibi nc nr nz n_past n_head scale in out: scale -> alibi -> mask -> softmax
+       (the BLOOM attention scores; ggml_alibi ggml.c:2949, 6184-6244) */
+    int nc = ARG(2), nr = ARG(3), nz = ARG(4), n_past = ARG(5), n_head = ARG(6);
+    float sc = (float)atof(argv[7]);
+    struct ggml_tensor *x = ggml_new_tensor_3d(ctx, GGML_TYPE_F32, nc, nr, nz);
+    void *xd = slurp(argv[8], ggml_nbytes(x)); memcpy(x->data, xd, ggml_nbytes(x));
+    struct ggml_tensor *y = ggml_soft_max(ctx, ggml_diag_mask_inf(ctx,
+        ggml_alibi(ctx, ggml_scale(ctx, x, ggml_new_f32(ctx, sc)), n_past, n_head), n_past));
+    run(ctx, y);
+    spit(argv[9], y->data, ggml_nbytes(y));
   } else if (!strcmp(op, "rope_neox") || !strcmp(op, "rope_gptj")) {
     /* rope_* d H T n_past n_dims mode in out        ggml.c:6086-6153 / 5919-5974 */
     int d = ARG(2), H = ARG(3), T = ARG(4), n_past = ARG(5), n_dims = ARG(6), mode = ARG(7);

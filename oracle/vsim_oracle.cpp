@@ -276,11 +276,32 @@ void kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int N, f
     }
 }
 
+// ggml.c:6184-6244 ggml_compute_forward_alibi_f32 on p[nz][nr][nc] (ne0 = nc keys, ne1 = nr
+// query rows, ne2 = nz heads): dst = (j+1)*m_k + src with the head slopes in float from
+// double pow (m0 = 2^(-8/n), m1 = 2^(-4/n), n = 2^floor(log2(n_head))).  As in the
+// reference, the bias depends on the query row j, not on the key position.
+void alibi(float *p, int nc, int nr, int nz, int n_head) {
+  const int n_heads_log2_floor = 1 << (int)std::floor(std::log2(n_head));
+  const float m0 = std::pow(2.0, -8.0 / n_heads_log2_floor);
+  const float m1 = std::pow(2.0, -4.0 / n_heads_log2_floor);
+  for (int k = 0; k < nz; ++k) {
+    const float m_k = k < n_heads_log2_floor ? (float)std::pow(m0, k + 1)
+                                             : (float)std::pow(m1, 2 * (k - n_heads_log2_floor) + 1);
+    for (int j = 0; j < nr; ++j)
+      for (int i = 0; i < nc; ++i) {
+        float *x = p + ((size_t)k * nr + j) * nc + i;
+        *x = (j + 1) * m_k + *x;
+      }
+  }
+}
+
 // ---- model --------------------------------------------------------------------------------
 struct Layer {
   std::vector<float> ln1_w, ln1_b, ln2_w, ln2_b;
   std::vector<uint8_t> wq, wk, wv, wo, wfc, wproj;
   std::vector<float> bq, bk, bv, bo, bfc, bproj;
+  std::vector<uint8_t> wqkv;  // BLOOM: fused [3E][E], rows q | k | v (the converter's order)
+  std::vector<float> bqkv;
 };
 
 struct Model {
@@ -289,6 +310,7 @@ struct Model {
   int n_ctx = 512;
   std::vector<uint8_t> wte, lmh;
   std::vector<float> lnf_w, lnf_b, lmh_b;
+  std::vector<float> emb_w, emb_b;  // BLOOM word_embeddings_layernorm
   std::vector<Layer> layers;
   std::vector<float> mem_k, mem_v;  // [L][n_ctx][E], vsim.cpp:349-366
 };
@@ -310,9 +332,15 @@ Model *load_model(const char *path, int arch, int n_ctx) {
   m->n_ctx = n_ctx;
   read_all(f, &m->n_vocab, 4);
   read_all(f, &m->n_embd, 4);
+  if (arch == VO_ARCH_BLOOM) {  // convert_bloom_to_ggml.py:79-85: vocab, hidden, multiple_of, heads, layers, ftype
+    int32_t n_mult = 0;
+    read_all(f, &n_mult, 4);
+    m->n_rot = 0;
+    m->par_res = 0;
+  }
   read_all(f, &m->n_head, 4);
   read_all(f, &m->n_layer, 4);
-  read_all(f, &m->n_rot, 4);
+  if (arch != VO_ARCH_BLOOM) read_all(f, &m->n_rot, 4);
   if (arch == VO_ARCH_GPTNEOX) read_all(f, &m->par_res, 4);
   read_all(f, &m->ftype, 4);
   int32_t nv = m->n_vocab;
@@ -352,6 +380,29 @@ Model *load_model(const char *path, int arch, int n_ctx) {
       f32slot(p + "mlp.dense_h_to_4h.bias", l.bfc, 4 * E);
       q4slot(p + "mlp.dense_4h_to_h.weight", l.wproj, (size_t)E * 4 * E);
       f32slot(p + "mlp.dense_4h_to_h.bias", l.bproj, E);
+    }
+  } else if (arch == VO_ARCH_BLOOM) {  // convert_bloom_to_ggml.py:22-34 names
+    q4slot("tok_embeddings.weight", m->wte, (size_t)E * V);
+    f32slot("norm.weight", m->emb_w, E);
+    f32slot("norm.bias", m->emb_b, E);
+    f32slot("output_norm.weight", m->lnf_w, E);
+    f32slot("output_norm.bias", m->lnf_b, E);
+    q4slot("output.weight", m->lmh, (size_t)E * V);
+    for (int i = 0; i < L; ++i) {
+      auto &l = m->layers[i];
+      const std::string p = "layers." + std::to_string(i) + ".";
+      f32slot(p + "attention_norm.weight", l.ln1_w, E);
+      f32slot(p + "attention_norm.bias", l.ln1_b, E);
+      q4slot(p + "attention.query_key_value.weight", l.wqkv, (size_t)E * 3 * E);
+      f32slot(p + "attention.query_key_value.bias", l.bqkv, 3 * E);
+      q4slot(p + "attention.wo.weight", l.wo, (size_t)E * E);
+      f32slot(p + "attention.wo.bias", l.bo, E);
+      f32slot(p + "ffn_norm.weight", l.ln2_w, E);
+      f32slot(p + "ffn_norm.bias", l.ln2_b, E);
+      q4slot(p + "feed_forward.w1.weight", l.wfc, (size_t)E * 4 * E);
+      f32slot(p + "feed_forward.w1.bias", l.bfc, 4 * E);
+      q4slot(p + "feed_forward.w2.weight", l.wproj, (size_t)E * 4 * E);
+      f32slot(p + "feed_forward.w2.bias", l.bproj, E);
     }
   } else {
     q4slot("transformer.wte.weight", m->wte, (size_t)E * V);
@@ -419,10 +470,75 @@ void add_bias(std::vector<float> &x, const std::vector<float> &b, int E, int N) 
     for (int i = 0; i < E; ++i) x[(size_t)t * E + i] = x[(size_t)t * E + i] + b[i];
 }
 
+// The BLOOM graph (no reference program composes it, SURVEY.md finding 2): the op sequence
+// of the bloomz.cpp-style graph the reference's converter and quantizer target
+// (convert_bloom_to_ggml.py, quantize_bloom.cpp), from reference ops only: embedding +
+// word_embeddings_layernorm; per layer LN -> fused QKV (+bias; rows q|k|v) -> KQ -> scale
+// -> ggml_alibi -> diag_mask_inf -> soft_max -> KQV -> wo (+bias) -> inpFF = attn + inpL
+// -> LN -> w1 (+bias) -> GELU -> w2 (+bias) -> inpL = ff + inpFF; output_norm; lm_head.
+void eval_bloom(Model &m, int n_past, const int32_t *tok, int N, float *logits, int nthreads) {
+  const int E = m.n_embd, H = m.n_head, d = E / H, L = m.n_layer, V = m.n_vocab, F = 4 * E;
+  const int n_ctx = m.n_ctx, nk = n_past + N;
+  std::vector<float> inpL((size_t)E * N), cur((size_t)E * N), qkv((size_t)3 * E * N), Q((size_t)E * N),
+      attn((size_t)E * N), inpFF((size_t)E * N), fch((size_t)F * N), ff((size_t)E * N);
+  std::vector<float> KQ((size_t)H * N * nk), KQV((size_t)H * N * d);
+  const size_t rbE = (size_t)E / QK * QBYTES;
+  for (int t = 0; t < N; ++t) dequantize_row(m.wte.data() + (size_t)tok[t] * rbE, cur.data() + (size_t)t * E, E);
+  for (int t = 0; t < N; ++t) norm_row(cur.data() + (size_t)t * E, inpL.data() + (size_t)t * E, E);
+  affine(inpL, m.emb_w, m.emb_b, E, N);
+  const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));  // as vsim.cpp:589
+  for (int il = 0; il < L; ++il) {
+    Layer &l = m.layers[il];
+    for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
+    affine(cur, l.ln1_w, l.ln1_b, E, N);
+    mul_mat_f(l.wqkv.data(), 3 * E, E, cur.data(), N, qkv.data(), nthreads);
+    add_bias(qkv, l.bqkv, 3 * E, N);
+    float *mk = m.mem_k.data() + (size_t)il * n_ctx * E;
+    float *mv = m.mem_v.data() + (size_t)il * n_ctx * E;
+    for (int t = 0; t < N; ++t) {  // views at offsets 0, E, 2E of each [3E] row
+      std::memcpy(Q.data() + (size_t)t * E, qkv.data() + (size_t)t * 3 * E, sizeof(float) * E);
+      std::memcpy(mk + (size_t)(n_past + t) * E, qkv.data() + (size_t)t * 3 * E + E, sizeof(float) * E);
+      std::memcpy(mv + (size_t)(n_past + t) * E, qkv.data() + (size_t)t * 3 * E + 2 * E, sizeof(float) * E);
+    }
+    kq(mk, E, Q.data(), E, d, H, nk, N, KQ.data());
+    for (auto &v : KQ) v *= scale;
+    alibi(KQ.data(), nk, N, H, H);
+    for (int h = 0; h < H; ++h)
+      for (int j = 0; j < N; ++j)
+        for (int i = n_past; i < nk; ++i)
+          if (i > n_past + j) KQ[((size_t)h * N + j) * nk + i] = -INFINITY;
+    for (int r = 0; r < H * N; ++r) soft_max_row(KQ.data() + (size_t)r * nk, nk);
+    kqv(mv, E, KQ.data(), d, H, nk, N, KQV.data());
+    for (int t = 0; t < N; ++t)
+      for (int h = 0; h < H; ++h)
+        for (int i = 0; i < d; ++i) cur[(size_t)t * E + h * d + i] = KQV[((size_t)h * N + t) * d + i];
+    mul_mat_f(l.wo.data(), E, E, cur.data(), N, attn.data(), nthreads);
+    add_bias(attn, l.bo, E, N);
+    for (size_t i = 0; i < inpFF.size(); ++i) inpFF[i] = attn[i] + inpL[i];
+    for (int t = 0; t < N; ++t) norm_row(inpFF.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
+    affine(cur, l.ln2_w, l.ln2_b, E, N);
+    mul_mat_f(l.wfc.data(), F, E, cur.data(), N, fch.data(), nthreads);
+    add_bias(fch, l.bfc, F, N);
+    gelu(fch.data(), fch.data(), F * N);
+    mul_mat_f(l.wproj.data(), E, F, fch.data(), N, ff.data(), nthreads);
+    add_bias(ff, l.bproj, E, N);
+    for (size_t i = 0; i < inpL.size(); ++i) inpL[i] = ff[i] + inpFF[i];
+  }
+  for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
+  affine(cur, m.lnf_w, m.lnf_b, E, N);
+  std::vector<float> lg((size_t)V * N);
+  mul_mat_f(m.lmh.data(), V, E, cur.data(), N, lg.data(), nthreads);
+  std::memcpy(logits, lg.data() + (size_t)V * (N - 1), sizeof(float) * V);
+}
+
 // vsim.cpp:470-747 (GPT-NeoX) ; the GPT-J graph is the same op sequence with ggml_rope
 // (ggml.c:5919-5974), one LayerNorm feeding attention and MLP, no q/k/v/out biases and a
 // biased lm_head.  Returns logits of the last token in `logits` (vsim.cpp:736-737).
 void eval(Model &m, int n_past, const int32_t *tok, int N, float *logits, int nthreads) {
+  if (m.arch == VO_ARCH_BLOOM) {
+    eval_bloom(m, n_past, tok, N, logits, nthreads);
+    return;
+  }
   const int E = m.n_embd, H = m.n_head, d = E / H, L = m.n_layer, V = m.n_vocab, F = 4 * E;
   const int n_ctx = m.n_ctx;
   const bool gptj = m.arch == VO_ARCH_GPTJ;
@@ -589,6 +705,7 @@ void vo_soft_max_f32(float *p, int nc, int nr) {
   for (int r = 0; r < nr; ++r) soft_max_row(p + (size_t)r * nc, nc);
 }
 void vo_scale_f32(float *p, int n, float v) { for (int i = 0; i < n; ++i) p[i] *= v; }
+void vo_alibi_f32(float *p, int nc, int nr, int nz, int n_head) { alibi(p, nc, nr, nz, n_head); }
 void vo_diag_mask_inf_f32(float *p, int nc, int nr, int nz, int n_past) {
   for (int k = 0; k < nz; k++)
     for (int j = 0; j < nr; j++)
@@ -668,7 +785,9 @@ void *vo_model_synthetic(int arch, int n_vocab, int n_embd, int n_head, int n_la
     q4(l.wfc, F, E); q4(l.wproj, E, F);
     f32(l.bq, E, 0.0f); f32(l.bk, E, 0.0f); f32(l.bv, E, 0.0f); f32(l.bo, E, 0.0f);
     f32(l.bfc, F, 0.0f); f32(l.bproj, E, 0.0f);
+    if (arch == VO_ARCH_BLOOM) { q4(l.wqkv, 3 * E, E); f32(l.bqkv, 3 * E, 0.0f); }
   }
+  if (arch == VO_ARCH_BLOOM) { f32(m->emb_w, E, 1.0f); f32(m->emb_b, E, 0.0f); m->par_res = 0; m->n_rot = 0; }
   m->mem_k.assign((size_t)n_layer * n_ctx * E, 0.0f);
   m->mem_v.assign((size_t)n_layer * n_ctx * E, 0.0f);
   return m;

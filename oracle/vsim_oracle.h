@@ -16,7 +16,10 @@
 extern "C" {
 #endif
 
-enum { VO_ARCH_GPTNEOX = 0, VO_ARCH_GPTJ = 1 };
+/* VO_ARCH_BLOOM: the BLOOM graph no reference program composes (SURVEY.md finding 2), built
+ * from reference ops incl. ggml_alibi (ggml.c:6184-6244); file format of
+ * converters/convert_bloom_to_ggml.py + quantize_bloom.cpp */
+enum { VO_ARCH_GPTNEOX = 0, VO_ARCH_GPTJ = 1, VO_ARCH_BLOOM = 2 };
 
 void     vo_init_tables(void);
 float    vo_fp16_to_fp32(uint16_t h);
@@ -36,6 +39,9 @@ void vo_gelu_f32(const float *x, float *y, int n);
 void vo_soft_max_f32(float *p, int nc, int nr);
 void vo_scale_f32(float *p, int n, float v);
 void vo_diag_mask_inf_f32(float *p, int nc, int nr, int nz, int n_past);
+/* ggml_alibi (ggml.c:6184-6244) on p[nz][nr][nc]: p += (row j + 1) * m_head, the head slopes
+ * of the reference (which depend on the query row j, not on the key column) */
+void vo_alibi_f32(float *p, int nc, int nr, int nz, int n_head);
 /* x: [T][H][d] float rows (ne0=d, ne1=H, ne2=T).  mode 0: p = n_past+i2 for all i2;
  * mode 1: only i2 >= n_past, p = i2. */
 void vo_rope_neox(float *x, int d, int H, int T, int n_past, int n_dims, int mode);

@@ -162,6 +162,24 @@ def gen_ops():
                         idx=idx, y=fread(tmp("y"), np.float32))
 
 
+def gen_alibi():
+    """scale -> ggml_alibi -> diag_mask_inf -> soft_max (the BLOOM score path; ggml_alibi
+    requires nc == nr + n_past, ggml.c:6215)."""
+    rng = np.random.Generator(np.random.PCG64(4321))
+    cases = {}
+    for ci, (nr, nz, n_past, sc) in enumerate([(3, 4, 4, 0.17677669), (1, 16, 40, 0.125), (9, 12, 0, 0.125),
+                                                (1, 16, 300, 0.125), (5, 6, 7, 0.25)]):
+        nc = nr + n_past
+        xa = (rng.standard_normal(nc * nr * nz) * 6).astype(np.float32)
+        xa.tofile(tmp("x"))
+        harness("attnsm_alibi", nc, nr, nz, n_past, nz, repr(sc), tmp("x"), tmp("y"))
+        cases[f"c{ci}_shape"] = np.array([nc, nr, nz, n_past], np.int32)
+        cases[f"c{ci}_scale"] = np.array([sc], np.float32)
+        cases[f"c{ci}_x"] = xa
+        cases[f"c{ci}_y"] = fread(tmp("y"), np.float32)
+    np.savez_compressed(os.path.join(OUT, "ops_attnsm_alibi.npz"), **cases)
+
+
 def run_vsim(model, prompt, extra):
     cmd = [VSIM, "gptneox", "-m", model, "--prompt", prompt, "--threads", "1", *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, check=True)
@@ -216,6 +234,10 @@ if __name__ == "__main__":
     for b in (HARNESS, VSIM):
         if not os.path.exists(b):
             sys.exit(f"missing {b}: run `make -C oracle ref` first")
+    if sys.argv[1:] == ["alibi"]:  # (added later: regenerates only the ALiBi vectors)
+        gen_alibi()
+        sys.exit(0)
     gen_ops()
+    gen_alibi()
     gen_e2e()
     print("fixtures written to", OUT)

@@ -39,6 +39,7 @@ def lib():
         L.vo_soft_max_f32.argtypes = [vp, ci, ci]
         L.vo_scale_f32.argtypes = [vp, ci, cf]
         L.vo_diag_mask_inf_f32.argtypes = [vp, ci, ci, ci, ci]
+        L.vo_alibi_f32.argtypes = [vp, ci, ci, ci, ci]
         L.vo_rope_neox.argtypes = [vp, ci, ci, ci, ci, ci, ci]
         L.vo_rope_gptj.argtypes = [vp, ci, ci, ci, ci, ci, ci]
         L.vo_kq.argtypes = [vp, ci, vp, ci, ci, ci, ci, ci, vp]
@@ -93,6 +94,17 @@ def attn_softmax(x, nc, nr, nz, n_past, scale):
     lib().vo_scale_f32(p(y), y.size, ctypes.c_float(scale))
     lib().vo_diag_mask_inf_f32(p(y), nc, nr, nz, n_past)
     lib().vo_soft_max_f32(p(y), nc, nr * nz)
+    return y
+
+
+def attn_softmax_alibi(x, nc, nr, nz, n_past, n_head, scale):
+    """scale -> ggml_alibi -> diag_mask_inf -> soft_max (the BLOOM score path)."""
+    y = np.ascontiguousarray(x, np.float32).copy()
+    L = lib()
+    L.vo_scale_f32(p(y), y.size, scale)
+    L.vo_alibi_f32(p(y), nc, nr, nz, n_head)
+    L.vo_diag_mask_inf_f32(p(y), nc, nr, nz, n_past)
+    L.vo_soft_max_f32(p(y), nc, nr * nz)
     return y
 
 

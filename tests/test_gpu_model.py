@@ -217,3 +217,31 @@ def test_fast_prefill_tracks_exact(tmp_path):
     lf = mf.eval(0, ids)
     cos = float(np.dot(le, lf) / (np.linalg.norm(le) * np.linalg.norm(lf)))
     assert cos > 0.95, cos
+
+
+@pytest.mark.parametrize("cfg", ["tiny-bloom", "small-bloom"])
+def test_bloom_bit_exact_vs_oracle(cfg, tmp_path):
+    """BLOOM: ALiBi, fused QKV, embedding LayerNorm, serial residual.
+    No reference program composes the BLOOM graph (finding 2), so model-level parity is
+    against the oracle's composition of reference ops; ggml_alibi itself is pinned to the
+    reference's op by tests/test_oracle_golden.py::test_scale_alibi_mask_softmax."""
+    arch_s, hp = mg.CONFIGS[cfg]
+    path = str(tmp_path / f"{cfg}.bin")
+    mg.write_model(path, arch_s, hp, seed=21, std=0.05)
+    _decode_compare(path, hip.ARCH_BLOOM, [4, 8, 15, 16, 23, 42], steps=12)
+
+
+def test_bloom_cli_greedy_matches_oracle(tmp_path):
+    """vsim-hip bloom ...: the front-end's argv (interface.py maps BLOOM to "bloom") and the
+    stdout token protocol, greedy tokens equal to the oracle's decode loop."""
+    import oracle_py as O
+    arch_s, hp = mg.CONFIGS["small-bloom"]
+    path = str(tmp_path / "sb.bin")
+    mg.write_model(path, arch_s, hp, seed=22, std=0.05)
+    prompt = [3, 1, 4, 1, 5]
+    out = run_cli(["bloom", "-m", path, "--prompt", " ".join(map(str, prompt)), "--n_predict", "16",
+                   "--top_k", "1", "--top_p", "1.0", "--temp", "1.0", "--repeat_penalty", "1.0", "--seed", "42",
+                   "--threads", "1"])
+    om = O.Model(path, 2)
+    want = om.generate(prompt, 16, seed=42, top_k=1, top_p=1.0, temp=1.0, repeat_penalty=1.0)
+    assert tokens(out) == list(want)

@@ -46,6 +46,29 @@ def test_scale_mask_softmax(c):
     assert np.array_equal(bits(y), bits(c["y"]))
 
 
+@pytest.mark.parametrize("c", cases(ops("attnsm_alibi")), ids=lambda c: "x".join(map(str, c["shape"])))
+def test_scale_alibi_mask_softmax(c):
+    """ggml_alibi (ggml.c:6184-6244) in the BLOOM score path, against the reference's op."""
+    nc, nr, nz, n_past = (int(v) for v in c["shape"])
+    y = O.attn_softmax_alibi(c["x"], nc, nr, nz, n_past, nz, float(c["scale"][0]))
+    assert np.array_equal(bits(y), bits(c["y"]))
+
+
+def test_bloom_graph_runs(tmp_path):
+    """The oracle's BLOOM graph (no reference program composes one: parity unpinned at the
+    model level, pinned per op) loads a synthetic ggml BLOOM file (the converter's header and
+    names) and decodes to finite logits."""
+    from vsim_amd import modelgen as mg
+    arch_s, hp = mg.CONFIGS["tiny-bloom"]
+    path = str(tmp_path / "tb.bin")
+    mg.write_model(path, arch_s, hp, seed=5, std=0.05)
+    m = O.Model(path, 2)  # VO_ARCH_BLOOM
+    lg = m.eval(0, [1, 2, 3])
+    assert lg.shape == (hp.n_vocab,) and np.all(np.isfinite(lg))
+    lg2 = m.eval(3, [int(np.argmax(lg))])
+    assert np.all(np.isfinite(lg2)) and not np.array_equal(lg, lg2)
+
+
 @pytest.mark.parametrize("style", ["neox", "gptj"])
 def test_rope(style):
     for c in cases(ops("rope_" + style)):

@@ -252,7 +252,11 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
                       hipStream_t s);
 int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
-int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s);
+int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s,
+                        const float *alibi = nullptr);
+// ggml_alibi head slopes (ggml.c:6217-6232), computed on the host with the reference's
+// double pow and float rounding
+void alibi_slopes_host(float *m, int n_head);
 int launch_rope(int style, float *x, int d, int H, int T, int n_past, int n_dims, int mode,
                 const double2 *cs, hipStream_t s);
 int launch_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq,

@@ -35,6 +35,8 @@ struct Slot {
 };
 
 struct LayerW {
+  // (BLOOM: wq/wk/wv are the three row blocks of the fused query_key_value tensor, each
+  // repacked on its own; bq/bk/bv point into its one bias vector)
   void *wq = nullptr, *wk = nullptr, *wv = nullptr, *wo = nullptr, *wfc = nullptr, *wproj = nullptr;
   float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
   float *bq = nullptr, *bk = nullptr, *bv = nullptr, *bo = nullptr, *bfc = nullptr, *bproj = nullptr;
@@ -57,6 +59,8 @@ struct vsim_model {
   std::vector<LayerW> layers;
   void *wte = nullptr, *lmh = nullptr;
   float *lnf_w = nullptr, *lnf_b = nullptr, *lmh_b = nullptr;
+  float *emb_w = nullptr, *emb_b = nullptr;  // BLOOM word_embeddings_layernorm
+  float *alibi = nullptr;                    // BLOOM: device head slopes [n_head]
 
   float *kcache = nullptr, *vcache = nullptr;
   double2 *rope_cs = nullptr;
@@ -246,6 +250,34 @@ void plan_slots(vsim_model *m, std::vector<std::pair<std::string, Slot>> &out) {
       q(p + "mlp.dense_4h_to_h.weight", E, F, i);
       f(p + "mlp.dense_4h_to_h.bias", E, i);
     }
+  } else if (m->arch == VSIM_ARCH_BLOOM) {  // convert_bloom_to_ggml.py:22-34 names
+    if (m->first) {
+      q("tok_embeddings.weight", V, E, -1);
+      f("norm.weight", E, -1);
+      f("norm.bias", E, -1);
+    }
+    if (m->last) {
+      f("output_norm.weight", E, -1);
+      f("output_norm.bias", E, -1);
+      q("output.weight", V, E, -1);
+    }
+    for (int i = m->l0; i < m->l1; ++i) {
+      const std::string p = "layers." + std::to_string(i) + ".";
+      f(p + "attention_norm.weight", E, i);
+      f(p + "attention_norm.bias", E, i);
+      q(p + "attention.query_key_value.weight/q", E, E, i);  // the file tensor's row blocks
+      q(p + "attention.query_key_value.weight/k", E, E, i);
+      q(p + "attention.query_key_value.weight/v", E, E, i);
+      f(p + "attention.query_key_value.bias", 3 * E, i);
+      q(p + "attention.wo.weight", E, E, i);
+      f(p + "attention.wo.bias", E, i);
+      f(p + "ffn_norm.weight", E, i);
+      f(p + "ffn_norm.bias", E, i);
+      q(p + "feed_forward.w1.weight", F, E, i);
+      f(p + "feed_forward.w1.bias", F, i);
+      q(p + "feed_forward.w2.weight", E, F, i);
+      f(p + "feed_forward.w2.bias", E, i);
+    }
   } else {
     if (m->first) q("transformer.wte.weight", V, E, -1);
     if (m->last) {
@@ -308,6 +340,34 @@ void bind_pointers(vsim_model *m) {
       L.wproj = P(p + "mlp.dense_4h_to_h.weight");
       L.bproj = F(p + "mlp.dense_4h_to_h.bias");
     }
+  } else if (m->arch == VSIM_ARCH_BLOOM) {
+    m->wte = P("tok_embeddings.weight");
+    m->emb_w = F("norm.weight");
+    m->emb_b = F("norm.bias");
+    m->lnf_w = F("output_norm.weight");
+    m->lnf_b = F("output_norm.bias");
+    m->lmh = P("output.weight");
+    const int E = m->hp.n_embd;
+    for (int i = m->l0; i < m->l1; ++i) {
+      LayerW &L = m->layers[i - m->l0];
+      const std::string p = "layers." + std::to_string(i) + ".";
+      L.ln1_w = F(p + "attention_norm.weight");
+      L.ln1_b = F(p + "attention_norm.bias");
+      L.ln2_w = F(p + "ffn_norm.weight");
+      L.ln2_b = F(p + "ffn_norm.bias");
+      L.wq = P(p + "attention.query_key_value.weight/q");
+      L.wk = P(p + "attention.query_key_value.weight/k");
+      L.wv = P(p + "attention.query_key_value.weight/v");
+      L.bq = F(p + "attention.query_key_value.bias");
+      L.bk = L.bq + E;
+      L.bv = L.bq + 2 * E;
+      L.wo = P(p + "attention.wo.weight");
+      L.bo = F(p + "attention.wo.bias");
+      L.wfc = P(p + "feed_forward.w1.weight");
+      L.bfc = F(p + "feed_forward.w1.bias");
+      L.wproj = P(p + "feed_forward.w2.weight");
+      L.bproj = F(p + "feed_forward.w2.bias");
+    }
   } else {
     m->wte = P("transformer.wte.weight");
     m->lnf_w = F("transformer.ln_f.weight");
@@ -366,7 +426,41 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
   return VSIM_OK;
 }
 
+// The BLOOM layer (oracle eval_bloom): LN -> q/k/v (+bias) -> KV write -> KQ -> scale ->
+// alibi -> mask -> softmax -> KQV -> wo (+bias) -> inpFF = attn + inpL -> LN -> w1 (+bias) ->
+// GELU -> w2 (+bias) -> inpL = ff + inpFF.
+int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
+  const LayerW &L = m->layers[il - m->l0];
+  const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E;
+  hipStream_t s = m->stream;
+  RC(launch_norm(m->inpL, m->cur1, E, N, L.ln1_w, L.ln1_b, s)); ++nk;
+  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, L.bq, m->Qb, nk));
+  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bk, m->Kb, nk));
+  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bv, m->Vb, nk));
+  const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
+  float *kc = m->kcache + loff, *vc = m->vcache + loff;
+  RC(launch_rope_kv_write(0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, 0, m->rope_cs, s)); ++nk;  // no rotary
+  const int nkv = n_past + N;
+  const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
+  RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s, m->alibi)); ++nk;
+  RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
+  RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, L.bo, m->attn, nk));
+  // inpFF = attn + inpL (kept in cur2), its LayerNorm into cur1
+  VSIM_HIP(hipMemcpyAsync(m->cur2, m->attn, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+  RC(launch_add_bias(m->cur2, m->inpL, N * E, 1, s)); ++nk;
+  RC(launch_norm(m->cur2, m->cur1, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
+  RC(mm(m, L.wfc, F, E, m->cur1, N, m->xq2, m->xd2, true, nullptr, m->fch, nk));
+  RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
+  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk));
+  // inpL = ff + inpFF
+  VSIM_HIP(hipMemcpyAsync(m->inpL, m->cur2, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
+  RC(launch_add_bias(m->inpL, m->ff, N * E, 1, s)); ++nk;
+  return VSIM_OK;
+}
+
 int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
+  if (m->arch == VSIM_ARCH_BLOOM) return run_layer_bloom(m, il, n_past, N, nk);
   const LayerW &L = m->layers[il - m->l0];
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E;
   const bool gptj = m->arch == VSIM_ARCH_GPTJ;
@@ -445,13 +539,16 @@ double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 // the same replayable form as enqueue_decode (token and n_past from device memory).
 // Shapes the fast step handles: head dim a multiple of 32 up to 256, rotary pairs inside one
 // 32-row tile (GPT-J pairs; GPT-NeoX rotate-half with n_rot <= 32), n_embd <= 8192.
-// fc_out K splits: FD_SF, or VSIM_FAST_SF (1, 2, 4 or 8; A/B timing)
-int fast_sf() {
-  static const int sf = [] {
+// fc_out K splits: FD_SF (or VSIM_FAST_SF = 1, 2, 4 or 8; A/B timing), doubled until one
+// split's activation slice fits the LDS staging (at most FD_MAXE values)
+int fast_sf(const vsim_model *m) {
+  static const int sf0 = [] {
     const char *e = getenv("VSIM_FAST_SF");
     const int v = e ? atoi(e) : FD_SF;
     return v == 1 || v == 2 || v == 4 || v == 8 ? v : FD_SF;
   }();
+  int sf = sf0;
+  while (sf < 8 && 4 * m->hp.n_embd / sf > FD_MAXE) sf *= 2;
   return sf;
 }
 
@@ -527,7 +624,7 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     T.xf_qs = q3;
     T.xf_d = d3;
     T.ffp = m->fast_ffp;
-    T.sf = fast_sf();
+    T.sf = fast_sf(m);
     T.q = m->Qb;
     T.kc = m->kcache + loff;
     T.vc = m->vcache + loff;
@@ -550,7 +647,7 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     O.nchunk = nchunk;
     O.bo = gptj ? nullptr : L.bo;
     O.ffp = m->fast_ffp;
-    O.sf = fast_sf();
+    O.sf = fast_sf(m);
     O.bproj = L.bproj;
     O.x = R[cur];
     O.out = R[cur ^ 1];
@@ -826,7 +923,10 @@ size_t vsim_q4_bytes(int rows, int k) { return w4_bytes(rows, k); }
 int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
                       vsim_model **out) {
   if (!hp || !out) { set_error("model_create: null argument"); return VSIM_EINVAL; }
-  if (arch != VSIM_ARCH_GPTNEOX && arch != VSIM_ARCH_GPTJ) { set_error("model_create: unknown arch"); return VSIM_EINVAL; }
+  if (arch != VSIM_ARCH_GPTNEOX && arch != VSIM_ARCH_GPTJ && arch != VSIM_ARCH_BLOOM) {
+    set_error("model_create: unknown arch");
+    return VSIM_EINVAL;
+  }
   if (hp->n_embd % hp->n_head || hp->n_embd % 128 || hp->n_rot > hp->n_embd / hp->n_head || hp->n_rot % 2 ||
       n_ctx <= 0) {
     set_error("model_create: unsupported hparams (n_embd % 128, n_rot <= head dim, even n_rot)");
@@ -884,6 +984,15 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   if (hipMalloc((void **)&m->rope_cs, cs.size() * sizeof(double2)) != hipSuccess) return fail(VSIM_ENOMEM);
   if (hipMemcpy(m->rope_cs, cs.data(), cs.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
     return fail(hip_fail(hipErrorUnknown, "rope table upload"));
+  if (arch == VSIM_ARCH_BLOOM) {
+    m->hp.n_rot = 0;
+    m->hp.use_parallel_residual = 0;
+    std::vector<float> sl(hp->n_head);
+    alibi_slopes_host(sl.data(), hp->n_head);
+    if (hipMalloc((void **)&m->alibi, sl.size() * sizeof(float)) != hipSuccess) return fail(VSIM_ENOMEM);
+    if (hipMemcpy(m->alibi, sl.data(), sl.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(hip_fail(hipErrorUnknown, "alibi slopes upload"));
+  }
   DevTables t;
   if (int rc = tables_get(&t)) return fail(rc);
   if (int rc = ensure_scratch(m, 16)) return fail(rc);
@@ -895,6 +1004,7 @@ void vsim_model_free(vsim_model *m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
   if (m->stream) (void)hipStreamSynchronize(m->stream);
+  if (m->alibi) (void)hipFree(m->alibi);
   free_scratch(m);
   if (m->warena) (void)hipFree(m->warena);
   if (m->kcache) (void)hipFree(m->kcache);
@@ -908,6 +1018,16 @@ void vsim_model_free(vsim_model *m) {
 }
 
 int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes) {
+  {  // BLOOM's fused query_key_value weight: three [E][E] row blocks, q | k | v
+    const std::string n(name), suf = "attention.query_key_value.weight";
+    if (m->arch == VSIM_ARCH_BLOOM && n.size() >= suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0) {
+      const char *parts[3] = {"/q", "/k", "/v"};
+      if (nbytes % 3 != 0) { set_error("set_tensor: fused qkv size"); return VSIM_EINVAL; }
+      for (int i = 0; i < 3; ++i)
+        RC(vsim_model_set_tensor(m, (n + parts[i]).c_str(), (const uint8_t *)host + i * (nbytes / 3), nbytes / 3));
+      return VSIM_OK;
+    }
+  }
   auto it = m->slots.find(name);
   if (it == m->slots.end()) { set_error(std::string("set_tensor: unknown tensor ") + name); return VSIM_EINVAL; }
   Slot &s = it->second;
@@ -956,8 +1076,16 @@ int vsim_model_load_file(const char *path, int arch, int n_ctx, int device, int 
   if (!rd(&magic, 4) || magic != 0x67676d6c) { set_error("load: bad magic"); return VSIM_EFILE; }
   vsim_hparams hp{};
   int32_t ftype = 0;
-  rd(&hp.n_vocab, 4); rd(&hp.n_embd, 4); rd(&hp.n_head, 4); rd(&hp.n_layer, 4); rd(&hp.n_rot, 4);
-  hp.use_parallel_residual = 1;
+  rd(&hp.n_vocab, 4); rd(&hp.n_embd, 4);
+  if (arch == VSIM_ARCH_BLOOM) {  // convert_bloom_to_ggml.py:79-85: ..., multiple_of, n_head, n_layer, ftype
+    int32_t n_mult = 0;
+    rd(&n_mult, 4);
+    rd(&hp.n_head, 4); rd(&hp.n_layer, 4);
+    hp.n_rot = 0;
+  } else {
+    rd(&hp.n_head, 4); rd(&hp.n_layer, 4); rd(&hp.n_rot, 4);
+  }
+  hp.use_parallel_residual = arch == VSIM_ARCH_BLOOM ? 0 : 1;
   if (arch == VSIM_ARCH_GPTNEOX) rd(&hp.use_parallel_residual, 4);
   rd(&ftype, 4);
   if (ftype != 2) { set_error("load: only Q4_0 (f16 == 2) files are supported"); return VSIM_EFILE; }
@@ -985,6 +1113,7 @@ int vsim_model_load_file(const char *path, int arch, int n_ctx, int device, int 
     const size_t nbytes = ft == 0 ? ne * 4 : (ft == 2 ? ne / QK * QBYTES : 0);
     if (nbytes == 0) { vsim_model_free(m); set_error("load: unsupported tensor type in " + name); return VSIM_EFILE; }
     auto it = m->slots.find(name);
+    if (it == m->slots.end()) it = m->slots.find(name + "/q");  // BLOOM fused qkv
     if (it == m->slots.end()) {  // tensor of another pipeline stage
       f.seekg(nbytes, std::ios::cur);
       continue;
@@ -1214,8 +1343,14 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
         m->tok_host[i] = tokens[i];
       }
       VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->tok_host, N * sizeof(int32_t), hipMemcpyHostToDevice, s));
-      RC(launch_get_rows(m->wte, E, V, m->tok_dev, N, m->inpL, s));
-      ++nk;
+      if (m->arch == VSIM_ARCH_BLOOM) {  // word embeddings + word_embeddings_layernorm
+        RC(launch_get_rows(m->wte, E, V, m->tok_dev, N, m->cur1, s));
+        RC(launch_norm(m->cur1, m->inpL, E, N, m->emb_w, m->emb_b, s));
+        nk += 2;
+      } else {
+        RC(launch_get_rows(m->wte, E, V, m->tok_dev, N, m->inpL, s));
+        ++nk;
+      }
     } else {
       if (!resid_in) { set_error("eval: non-first stage needs resid_in"); return VSIM_EINVAL; }
       VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));

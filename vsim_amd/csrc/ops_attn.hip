@@ -25,6 +25,14 @@ void rope_table_host(double2 *cs, int n_pos, int n_dims) {
   }
 }
 
+void alibi_slopes_host(float *m, int n_head) {
+  const int n_heads_log2_floor = 1 << (int)floor(log2(n_head));
+  const float m0 = pow(2.0, -8.0 / n_heads_log2_floor);
+  const float m1 = pow(2.0, -4.0 / n_heads_log2_floor);
+  for (int k = 0; k < n_head; ++k)
+    m[k] = k < n_heads_log2_floor ? (float)pow(m0, k + 1) : (float)pow(m1, 2 * (k - n_heads_log2_floor) + 1);
+}
+
 // one thread per rotated pair; x[T][H][d]
 __device__ __forceinline__ void rope_pair(float *v, int style, int j, int n_dims, double2 c) {
   if (style == 0) {
@@ -144,17 +152,22 @@ int launch_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, in
 
 // scale -> mask -> softmax, one 256-thread block per row of nc (row r = (z, j)).
 // The fp16-valued exps sum exactly in double in any order (multiples of 2^-24, < 2^11).
+// alibi (BLOOM, may be null): per-head slopes m_k; after the scale each score gets
+// (j+1)*m_k added, j the query row (ggml_alibi, ggml.c:6184-6244), before the mask.
 __global__ void __launch_bounds__(256) k_attn_softmax(float *p, int nc, int nr, int n_past, float scale,
-                                                       const uint16_t *__restrict__ etab) {
+                                                       const uint16_t *__restrict__ etab,
+                                                       const float *__restrict__ alibi) {
   __shared__ float shf[4];
   __shared__ double shd[4];
   const int row = blockIdx.x;
   const int j = row % nr;
   float *x = p + (size_t)row * nc;
+  const float ab = alibi ? (float)(j + 1) * alibi[row / nr] : 0.0f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float mx = -INFINITY;
   for (int i = threadIdx.x; i < nc; i += 256) {
     float v = x[i] * scale;
+    if (alibi) v = ab + v;
     if (i >= n_past && i > n_past + j) v = -INFINITY;
     x[i] = v;
     mx = mx > v ? mx : v;
@@ -181,10 +194,11 @@ __global__ void __launch_bounds__(256) k_attn_softmax(float *p, int nc, int nr, 
   for (int i = threadIdx.x; i < nc; i += 256) x[i] = x[i] * inv;
 }
 
-int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s) {
+int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s,
+                        const float *alibi) {
   DevTables t;
   if (int rc = tables_get(&t)) return rc;
-  hipLaunchKernelGGL(k_attn_softmax, dim3(nr * nz), dim3(256), 0, s, p, nc, nr, n_past, scale, t.exp_f16);
+  hipLaunchKernelGGL(k_attn_softmax, dim3(nr * nz), dim3(256), 0, s, p, nc, nr, n_past, scale, t.exp_f16, alibi);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

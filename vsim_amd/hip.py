@@ -19,6 +19,7 @@ MODE_EXACT = 0
 MODE_FAST = 1
 ARCH_GPTNEOX = 0
 ARCH_GPTJ = 1
+ARCH_BLOOM = 2
 
 # symbols declared in include/vsim_hip.h (checked by tests/test_capi.py)
 EXPORTS = [

@@ -42,7 +42,7 @@ struct Params {
 };
 
 void usage(const char *argv0, const Params &p) {
-  fprintf(stderr, "usage: %s <gptneox|gptj> [options]\n\n", argv0);
+  fprintf(stderr, "usage: %s <gptneox|gptj|codegen|bloom> [options]\n\n", argv0);
   fprintf(stderr, "options:\n");
   fprintf(stderr, "  -h, --help            show this help message and exit\n");
   fprintf(stderr, "  -s SEED, --seed SEED  RNG seed (default: -1)\n");
@@ -273,6 +273,7 @@ int main(int argc, char **argv) {
   }
   if (model_type == "gptneox") return run(params, VSIM_ARCH_GPTNEOX);
   if (model_type == "gptj" || model_type == "codegen") return run(params, VSIM_ARCH_GPTJ);
+  if (model_type == "bloom") return run(params, VSIM_ARCH_BLOOM);  // interface.py:92-128 maps BLOOM here
   printf("Unknown model type: %s\n", model_type.c_str());
   return 1;
 }

@@ -79,6 +79,10 @@ CONFIGS = {
     "small-neox": ("gptneox", HParams(512, 512, 8, 2, 32)),
     "tiny-gptj": ("gptj", HParams(128, 128, 4, 2, 16)),
     "small-gptj": ("gptj", HParams(512, 512, 4, 2, 64)),
+    # BLOOM (ALiBi, no rotary: n_rot 0; serial residual; header n_mult = 1)
+    "bloom-560m": ("bloom", HParams(250880, 1024, 16, 24, 0, 0)),
+    "tiny-bloom": ("bloom", HParams(128, 128, 4, 2, 0, 0)),
+    "small-bloom": ("bloom", HParams(512, 512, 8, 2, 0, 0)),
 }
 
 
@@ -131,6 +135,29 @@ def tensor_specs(arch: str, hp: HParams):
         s.append(("transformer.ln_f.bias", [E], "b"))
         s.append(("lm_head.weight", [E, V], "q"))
         s.append(("lm_head.bias", [V], "b"))
+    elif arch == "bloom":  # convert_bloom_to_ggml.py:22-34 names, q|k|v rows fused
+        s.append(("tok_embeddings.weight", [E, V], "q"))
+        s.append(("norm.weight", [E], "w"))
+        s.append(("norm.bias", [E], "b"))
+        for i in range(L):
+            p = f"layers.{i}."
+            s += [
+                (p + "attention_norm.weight", [E], "w"),
+                (p + "attention_norm.bias", [E], "b"),
+                (p + "attention.query_key_value.weight", [E, 3 * E], "q"),
+                (p + "attention.query_key_value.bias", [3 * E], "b"),
+                (p + "attention.wo.weight", [E, E], "q"),
+                (p + "attention.wo.bias", [E], "b"),
+                (p + "ffn_norm.weight", [E], "w"),
+                (p + "ffn_norm.bias", [E], "b"),
+                (p + "feed_forward.w1.weight", [E, F], "q"),
+                (p + "feed_forward.w1.bias", [F], "b"),
+                (p + "feed_forward.w2.weight", [F, E], "q"),
+                (p + "feed_forward.w2.bias", [E], "b"),
+            ]
+        s.append(("output_norm.weight", [E], "w"))
+        s.append(("output_norm.bias", [E], "b"))
+        s.append(("output.weight", [E, V], "q"))
     else:
         raise ValueError(arch)
     return s
@@ -156,6 +183,8 @@ def write_model(path: str, arch: str, hp: HParams, seed: int = 0, std: float = 0
         if arch == "gptneox":
             f.write(struct.pack("<7i", hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot,
                                 hp.use_parallel_residual, hp.ftype))
+        elif arch == "bloom":  # convert_bloom_to_ggml.py:79-85 (multiple_of = 1)
+            f.write(struct.pack("<6i", hp.n_vocab, hp.n_embd, 1, hp.n_head, hp.n_layer, hp.ftype))
         else:
             f.write(struct.pack("<6i", hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot, hp.ftype))
             f.write(struct.pack("<i", hp.n_vocab))
@@ -190,6 +219,9 @@ def read_model(path: str, arch: str):
     if arch == "gptneox":
         nv, ne_, nh, nl, nr, pr, ft = i32(7)
         nvv = nv
+    elif arch == "bloom":
+        nv, ne_, _mult, nh, nl, ft = i32(6)
+        nr, pr, nvv = 0, 0, nv
     else:
         nv, ne_, nh, nl, nr, ft = i32(6)
         pr = 1
