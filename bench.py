@@ -37,6 +37,7 @@ from vsim_amd import pipeline  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s measured copy
 PROMPT = [50278, 12092, 2, 0, 50281]
+ARCHS = {"gptj": hip.ARCH_GPTJ, "gptneox": hip.ARCH_GPTNEOX, "bloom": hip.ARCH_BLOOM}
 # name parts of the Q4_0 GEMV launches (k_layer_tail: fc_out + out-projection, with the
 # attention heads running beside them in the same launch)
 GEMV_KERNELS = ("k_gemv_chain", "k_gemv_solo", "k_layer_tail", "k_gemv_fast")
@@ -70,6 +71,13 @@ def pmc_traffic_per_launch(path=None, mode="exact"):
     return sum(vals) / len(vals) if vals else None
 
 
+def metric_name(config: str) -> str:
+    """BASELINE.json's metric for the headline config; the same wording for the others."""
+    if config == "gpt-j-6B":
+        return "decode tokens/sec GPT-J-6B Q4_0 @1 GPU; achieved HBM GB/s vs peak"
+    return f"decode tokens/sec {config} Q4_0; achieved HBM GB/s vs peak"
+
+
 def q4_weight_bytes(arch: str, hp: mg.HParams) -> float:
     """B_w per decode token: every Q4_0 matrix incl. lm_head, 0.625 B/w."""
     E, F, L, V = hp.n_embd, hp.n_ff, hp.n_layer, hp.n_vocab
@@ -80,7 +88,7 @@ def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12):
     """CPU oracle (port of the reference path) on a bounded sample, tokens/s extrapolated."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
-    arch = 1 if arch_s == "gptj" else 0
+    arch = {"gptneox": 0, "gptj": 1, "bloom": 2}[arch_s]  # VO_ARCH_*
     nth = max(1, min(16, os.cpu_count() or 1))
     ctx = 5 + n_tokens + 1
 
@@ -155,7 +163,7 @@ def run_pipeline(args, world, rank, dev, dist):
     is that stream's tokens/s (strong scaling: the work per token is fixed)."""
     import torch
     arch_s, hp = mg.CONFIGS[args.config]
-    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    arch = ARCHS[arch_s]
     L = hp.n_layer
     per = (L + world - 1) // world
     l0, l1 = pipeline.layer_range(L, world, rank)
@@ -213,7 +221,7 @@ def run_pipeline(args, world, rank, dev, dist):
     value = args.steps / elapsed
     bw = q4_weight_bytes(arch_s, hp)
     line = {
-        "metric": "decode tokens/sec GPT-J-6B Q4_0 @1 GPU; achieved HBM GB/s vs peak",
+        "metric": metric_name(args.config),
         "value": round(value, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32 (Q4_0 x Q4_0 operands)",
@@ -240,7 +248,7 @@ def run_prefill(args, dev):
     (gemm_f16.hip); attention and the elementwise ops on the general-path kernels."""
     import torch
     arch_s, hp = mg.CONFIGS[args.config]
-    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    arch = ARCHS[arch_s]
     N = args.prefill
     model = hip.Model.create(arch, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
                                         n_layer=hp.n_layer, n_rot=hp.n_rot,
@@ -280,7 +288,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=248)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--config", default="gpt-j-6B", choices=["gpt-j-6B", "pythia-12b", "gpt-neoxt-20b",
+    ap.add_argument("--config", default="gpt-j-6B", choices=["gpt-j-6B", "pythia-12b", "gpt-neoxt-20b", "bloom-560m",
                                                               "codegen-16B"])
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--no-graph", action="store_true")
@@ -316,7 +324,7 @@ def main():
         return
 
     arch_s, hp = mg.CONFIGS[args.config]
-    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    arch = ARCHS[arch_s]
     n_ctx = max(512, len(PROMPT) + args.warmup + args.steps + 96)
     model = hip.Model.create(arch, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
                                         n_layer=hp.n_layer, n_rot=hp.n_rot,
@@ -335,7 +343,11 @@ def main():
         # the next without a host round trip; the same tokens as eval() + numpy.argmax
         # (tests/test_gpu_model.py::test_generate_matches_stepwise_greedy)
         nonlocal n_past, tok
-        if k:
+        if k and arch == hip.ARCH_BLOOM:  # serial residual: general path, host argmax
+            for _ in range(k):
+                tok = int(np.argmax(model.eval(n_past, [tok])))
+                n_past += 1
+        elif k:
             tok = model.generate(n_past, tok, k)[-1]
             n_past += k
 
@@ -393,7 +405,7 @@ def main():
     bw = q4_weight_bytes(arch_s, hp)
     info = model.info()
     line = {
-        "metric": "decode tokens/sec GPT-J-6B Q4_0 @1 GPU; achieved HBM GB/s vs peak",
+        "metric": metric_name(args.config),
         "value": round(value, 3),
         "unit": "tokens/s",
         "n_gpus": world,
@@ -414,7 +426,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_fast and args.mode == "exact":
+    if rank == 0 and world == 1 and not args.no_fast and args.mode == "exact" and arch != hip.ARCH_BLOOM:
         # (rewinds to the end of the warm-up: positions are overwritten, n_ctx bounds the rest)
         line["fast_mode"] = fast_companion(model, start[0], start[1], args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
