@@ -1,3 +1,3 @@
-echo "== tests"; timeout -k 10 600 python3 -m pytest tests -x -q -m gpu 2>&1 | tail -3 || exit 1
-echo "== bench tail"; timeout -k 10 300 python3 bench.py --steps 64 --no-cpu-baseline --no-fast --no-profile 2>&1 | grep -v amdgpu.ids | tail -1 | cut -c1-220 || exit 1
-echo "== bench no tail"; VSIM_TAIL=0 timeout -k 10 300 python3 bench.py --steps 64 --no-cpu-baseline --no-fast --no-profile 2>&1 | grep -v amdgpu.ids | tail -1 | cut -c1-220
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pf -o pf -- python3 $GRAFT_REPO_ROOT/bench.py --config codegen-16B --prefill 2048 > $GRAFT_REPO_ROOT/gpurun_out/pf.log 2>&1 || exit 1
+f=$(find $GRAFT_REPO_ROOT/gpurun_out/pf -name "*kernel_stats.csv" | head -1); cut -d, -f1-5 "$f" | head -14

@@ -29,22 +29,63 @@ typedef float af32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int AP_BQ = 128, AP_BK = 64, AP_THREADS = 256;
 
+// Keys [0, nk) of this layer's F32 cache as fp16, once per prompt eval: K16[key][E]
+// (row-major, as the cache) and Vt16[h][dim][ldt] (each head's V transposed, keys padded
+// with zeros to ldt, a multiple of AP_BK), so the attention workgroups stage both operand
+// tiles with 16-byte loads and stores.  64 keys x 64 columns per workgroup; V goes through
+// an LDS tile for the transpose.
+__global__ void __launch_bounds__(256) k_kv_f16(const float *__restrict__ kc, const float *__restrict__ vc, int E,
+                                                 int d, int nk, int ldt, _Float16 *__restrict__ k16,
+                                                 _Float16 *__restrict__ vt16) {
+  __shared__ float tv[64][65];
+  const int key0 = blockIdx.x * 64, col0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 64 * 16; e += 256) {  // 64 keys x 16 float4 columns
+    const int kk = e / 16, c4 = (e % 16) * 4, key = key0 + kk;
+    float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+    if (key < nk) {
+      kv = *(const float4 *)(kc + (size_t)key * E + col0 + c4);
+      vv = *(const float4 *)(vc + (size_t)key * E + col0 + c4);
+      ahalf4 hk = {(_Float16)kv.x, (_Float16)kv.y, (_Float16)kv.z, (_Float16)kv.w};
+      *(ahalf4 *)(k16 + (size_t)key * E + col0 + c4) = hk;
+    }
+    tv[kk][c4] = vv.x;
+    tv[kk][c4 + 1] = vv.y;
+    tv[kk][c4 + 2] = vv.z;
+    tv[kk][c4 + 3] = vv.w;
+  }
+  __syncthreads();
+  for (int e = tid; e < 64 * 16; e += 256) {  // 64 columns x 16 groups of 4 keys
+    const int cc = e / 16, k4 = (e % 16) * 4;
+    const int col = col0 + cc, h = col / d, dim = col % d;
+    ahalf4 hv = {(_Float16)tv[k4][cc], (_Float16)tv[k4 + 1][cc], (_Float16)tv[k4 + 2][cc], (_Float16)tv[k4 + 3][cc]};
+    if (key0 + k4 < ldt) *(ahalf4 *)(vt16 + ((size_t)h * d + dim) * ldt + key0 + k4) = hv;
+  }
+}
+
+// One workgroup = one head x 128 queries (4 waves of 32), keys in tiles of 64 through two
+// LDS buffers: the next tile's fp16 K rows and V^T rows load into registers (16-byte
+// chunks) while the current tile's MFMAs run.  Workgroups are ordered longest causal range
+// first (query block descending, heads interleaved) so the long ones do not start last.
 template <int D>
 __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__restrict__ Q,
-                                                                  const float *__restrict__ kc,
-                                                                  const float *__restrict__ vc, int E, int N,
-                                                                  int n_past, float qscale, float *__restrict__ out) {
+                                                                  const _Float16 *__restrict__ k16,
+                                                                  const _Float16 *__restrict__ vt16, int E, int H,
+                                                                  int N, int n_past, int ldt, float qscale,
+                                                                  float *__restrict__ out) {
   constexpr int KLD = D + 8;      // K tile [key][dim], halves
   constexpr int VLD = AP_BK + 8;  // V^T tile [dim][key], halves
   constexpr int NT = D / 32;      // O^T tiles (32 dims each)
-  __shared__ __attribute__((aligned(16))) _Float16 Ks[AP_BK * KLD];
-  __shared__ __attribute__((aligned(16))) _Float16 Vt[D * VLD];
-  const int h = blockIdx.y, q0 = blockIdx.x * AP_BQ;
+  constexpr int KCH = AP_BK * D / 8 / AP_THREADS;  // 16-byte chunks per thread per operand tile
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  // buffer b: K tile at lds + b * AP_BK * KLD, V^T tile at lds + 2 * AP_BK * KLD + b * D * VLD
+  const int nqb = (N + AP_BQ - 1) / AP_BQ;
+  const int h = blockIdx.x % H, q0 = (nqb - 1 - (int)blockIdx.x / H) * AP_BQ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hl = lane >> 5;
   const int qw = q0 + wave * 32;  // this wave's first query
   const int myq = qw + r;         // this lane's query (column of S^T / O^T)
-  const float *kbase = kc + (size_t)h * D, *vbase = vc + (size_t)h * D;
+  const _Float16 *kbase = k16 + (size_t)h * D, *vbase = vt16 + (size_t)h * D * ldt;
 
   // Q^T fragments: lane (query r, half hl) holds Q[q][16s + 8hl + j], j < 8, for every s
   ahalf8 qf[D / 16];
@@ -72,31 +113,69 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 
   const int klast = n_past + min(q0 + AP_BQ, N) - 1;  // last key any query of the block sees
   const int nkb = klast / AP_BK + 1;
-  for (int kb = 0; kb < nkb; ++kb) {
+  // tile staging: chunk c of thread t = 16 bytes; K: key c8 / (D/8), dims 8 * (c8 % (D/8));
+  // V^T: dim c8 / 8, keys 8 * (c8 % 8)
+  u32x4 rk[KCH], rv[KCH];
+  auto kload = [&](int kb) __attribute__((always_inline)) {
     const int k0 = kb * AP_BK;
-    // stage K (row-major) and V^T as fp16; keys past klast read as zero (masked below)
-    for (int e = tid; e < AP_BK * D / 4; e += AP_THREADS) {
-      const int key = e / (D / 4), c4 = (e % (D / 4)) * 4;
-      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k0 + key <= klast) kv = *(const float4 *)(kbase + (size_t)(k0 + key) * E + c4);
-      ahalf4 hk = {(_Float16)kv.x, (_Float16)kv.y, (_Float16)kv.z, (_Float16)kv.w};
-      *(ahalf4 *)&Ks[key * KLD + c4] = hk;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      const int c8 = tid + AP_THREADS * c;
+      const int key = k0 + c8 / (D / 8), col = 8 * (c8 % (D / 8));
+      rk[c] = *(const u32x4 *)(kbase + (size_t)min(key, klast) * E + col);
     }
-    for (int e = tid; e < AP_BK * D / 4; e += AP_THREADS) {
-      // consecutive threads take consecutive keys of one 4-dim group (conflict-light
-      // transposed stores)
-      const int key = e % AP_BK, c4 = (e / AP_BK) * 4;
-      float4 vv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k0 + key <= klast) vv = *(const float4 *)(vbase + (size_t)(k0 + key) * E + c4);
-      Vt[(c4 + 0) * VLD + key] = (_Float16)vv.x;
-      Vt[(c4 + 1) * VLD + key] = (_Float16)vv.y;
-      Vt[(c4 + 2) * VLD + key] = (_Float16)vv.z;
-      Vt[(c4 + 3) * VLD + key] = (_Float16)vv.w;
+  };
+  auto vload = [&](int kb) __attribute__((always_inline)) {
+    const int k0 = kb * AP_BK;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      const int c8 = tid + AP_THREADS * c;
+      rv[c] = *(const u32x4 *)(vbase + (size_t)(c8 / 8) * ldt + k0 + 8 * (c8 % 8));
     }
+  };
+  auto kstore = [&](int buf) __attribute__((always_inline)) {
+    _Float16 *Ks = lds + buf * AP_BK * KLD;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      const int c8 = tid + AP_THREADS * c;
+      *(u32x4 *)&Ks[(c8 / (D / 8)) * KLD + 8 * (c8 % (D / 8))] = rk[c];
+    }
+  };
+  auto vstore = [&](int buf) __attribute__((always_inline)) {
+    _Float16 *Vt = lds + 2 * AP_BK * KLD + buf * D * VLD;
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      const int c8 = tid + AP_THREADS * c;
+      *(u32x4 *)&Vt[(c8 / 8) * VLD + 8 * (c8 % 8)] = rv[c];
+    }
+  };
+  // D = 256: one LDS buffer, the tile staged at the top of each step (the register ring of
+  // the next tile does not fit beside the 256-dim Q fragments and O^T accumulators)
+  constexpr bool PF = D < 256;
+  if (PF) {
+    kload(0);
+    vload(0);
+    kstore(0);
+    vstore(0);
     __syncthreads();
-    if (k0 <= n_past + min(qw + 31, N - 1)) {  // wave-uniform: some key of the block is visible
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * AP_BK, buf = PF ? kb & 1 : 0;
+    const bool next = PF && kb + 1 < nkb;
+    if (!PF) {
+      kload(kb);
+      vload(kb);
+      kstore(0);
+      vstore(0);
+      __syncthreads();
+    }
+    // next tile: K rows load during this tile's S^T, V^T rows during its P·V
+    if (next) kload(kb + 1);
+    const _Float16 *Ks = lds + buf * AP_BK * KLD, *Vt = lds + 2 * AP_BK * KLD + buf * D * VLD;
+    const bool vis = k0 <= n_past + min(qw + 31, N - 1);  // wave-uniform: some key of the block is visible
+    af32x16 st[2];
+    if (vis) {
       // S^T tiles t = 0, 1 (keys k0 + 32t + row)
-      af32x16 st[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         st[t] = (af32x16){};
@@ -104,8 +183,17 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
         for (int s = 0; s < D / 16; ++s) {
           const ahalf8 kf = *(const ahalf8 *)&Ks[(32 * t + r) * KLD + 16 * s + 8 * hl];
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st[t], 0, 0, 0);
+          // (a scheduling fence every 4 steps: the compiler would otherwise hoist all the
+          // tile's LDS reads and run out of registers at D = 256)
+          if (D >= 256 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
       }
+    }
+    if (next) {
+      kstore(buf ^ 1);
+      vload(kb + 1);
+    }
+    if (vis) {
       // causal mask and the block maximum of this lane's query
       float bm = -INFINITY;
 #pragma unroll
@@ -148,9 +236,11 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
             const ahalf4 v0 = *(const ahalf4 *)vr, v1 = *(const ahalf4 *)(vr + 8);
             const ahalf8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
             o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
+            if (D >= 256 && (i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
           }
         }
     }
+    if (next) vstore(buf ^ 1);
     __syncthreads();
   }
   // O^T / l: lane = query, rows = dims (reg & 3) + 8 (reg >> 2) + 4 hl of tile i
@@ -170,20 +260,46 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 
 bool attn_prefill_supported(int d) { return d == 64 || d == 96 || d == 128 || d == 256; }
 
+template <int D>
+size_t attn_prefill_lds() {
+  const int nbuf = D < 256 ? 2 : 1;
+  return (size_t)(2 * AP_BK * (D + 8) + nbuf * D * (AP_BK + 8)) * sizeof(_Float16);
+}
+
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
-                            float scale, float *out, hipStream_t s) {
-  const int E = d * H;
-  const float qscale = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
-  const dim3 grid((N + AP_BQ - 1) / AP_BQ, H);
-  switch (d) {
-    case 64: hipLaunchKernelGGL(k_attn_prefill_f16<64>, grid, dim3(AP_THREADS), 0, s, Q, kc, vc, E, N, n_past, qscale, out); break;
-    case 96: hipLaunchKernelGGL(k_attn_prefill_f16<96>, grid, dim3(AP_THREADS), 0, s, Q, kc, vc, E, N, n_past, qscale, out); break;
-    case 128: hipLaunchKernelGGL(k_attn_prefill_f16<128>, grid, dim3(AP_THREADS), 0, s, Q, kc, vc, E, N, n_past, qscale, out); break;
-    case 256: hipLaunchKernelGGL(k_attn_prefill_f16<256>, grid, dim3(AP_THREADS), 0, s, Q, kc, vc, E, N, n_past, qscale, out); break;
-    default: set_error("attention prefill: head dim must be 64, 96, 128 or 256"); return VSIM_EINVAL;
+                            float scale, float *out, hipStream_t s, void *scratch, size_t scratch_bytes) {
+  if (!attn_prefill_supported(d)) {
+    set_error("attention prefill: head dim must be 64, 96, 128 or 256");
+    return VSIM_EINVAL;
   }
+  const int E = d * H, nk = n_past + N;
+  const int ldt = (nk + AP_BK - 1) / AP_BK * AP_BK;
+  const size_t need = attn_prefill_scratch(E, nk);
+  _Float16 *buf = (_Float16 *)scratch;
+  const bool own = !buf || scratch_bytes < need;
+  if (own) VSIM_HIP(hipMallocAsync((void **)&buf, need, s));
+  _Float16 *k16 = buf, *vt16 = buf + (size_t)ldt * E;
+  hipLaunchKernelGGL(k_kv_f16, dim3(ldt / 64, E / 64), dim3(256), 0, s, kc, vc, E, d, nk, ldt, k16, vt16);
+  const float qscale = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
+  const dim3 grid(((N + AP_BQ - 1) / AP_BQ) * H);
+#define APL(DD)                                                                                                   \
+  hipLaunchKernelGGL(k_attn_prefill_f16<DD>, grid, dim3(AP_THREADS), attn_prefill_lds<DD>(), s, Q, k16, vt16, E, H, \
+                     N, n_past, ldt, qscale, out)
+  switch (d) {
+    case 64: APL(64); break;
+    case 96: APL(96); break;
+    case 128: APL(128); break;
+    default: APL(256); break;
+  }
+#undef APL
   VSIM_HIP(hipGetLastError());
+  if (own) VSIM_HIP(hipFreeAsync(buf, s));
   return VSIM_OK;
+}
+
+size_t attn_prefill_scratch(int E, int nk) {
+  const size_t ldt = (size_t)(nk + AP_BK - 1) / AP_BK * AP_BK;
+  return 2 * ldt * E * sizeof(_Float16);
 }
 
 }  // namespace vsim

@@ -246,8 +246,11 @@ int launch_norm(const float *x, float *y, int k, int rows, const float *w, const
 int launch_argmax(const float *x, int n, int *out, hipStream_t s);
 int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s);
 bool attn_prefill_supported(int d);
+// scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
+// smaller: allocated stream-ordered per call)
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
-                            float scale, float *out, hipStream_t s);
+                            float scale, float *out, hipStream_t s, void *scratch = nullptr, size_t scratch_bytes = 0);
+size_t attn_prefill_scratch(int E, int nk);
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
                       hipStream_t s);
 int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);

@@ -54,8 +54,19 @@ __device__ __forceinline__ void deq_block_f16(uint4 q, float d, half8 out[4]) {
   }
 }
 
-__global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const uint8_t *__restrict__ xqs,
-                                                             const float *__restrict__ xdd, int N,
+// The activation rows dequantized once per GEMM call (the same halves the in-GEMM dequant
+// produced): X16[token][K], block i = token * nb + b at X16 + 32 i.
+__global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__ xqs, const float *__restrict__ xdd,
+                                                      size_t nblk, half8 *__restrict__ X16) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nblk) return;
+  half8 h[4];
+  deq_block_f16(*(const uint4 *)(xqs + i * 16), xdd[i], h);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) X16[4 * i + w] = h[w];
+}
+
+__global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16 *__restrict__ X16, int N,
                                                              const float *__restrict__ bias, float *__restrict__ Y) {
   __shared__ __attribute__((aligned(16))) _Float16 As[GM_BM * GM_LD];
   __shared__ __attribute__((aligned(16))) _Float16 Bs[GM_BN * GM_LD];
@@ -78,16 +89,12 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const uint8_t 
       d = 0.0f;
     }
   };
-  auto ldX = [&](int kb, uint4 &q, float &d) {
+  auto ldX = [&](int kb, u32x4 *xv) {  // the 32 halves of block kb + ub of token ntok
     const int b = kb + ub;
-    if (nok && b < nb) {
-      const size_t o = (size_t)ntok * nb + b;
-      q = *(const uint4 *)(xqs + o * 16);
-      d = xdd[o];
-    } else {
-      q = make_uint4(0x88888888u, 0x88888888u, 0x88888888u, 0x88888888u);
-      d = 0.0f;
-    }
+    const bool ok = nok && b < nb;
+    const u32x4 *src = (const u32x4 *)(X16 + ((size_t)(ok ? ntok : 0) * nb + (ok ? b : 0)) * 32);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) xv[w] = ok ? src[w] : u32x4{0u, 0u, 0u, 0u};
   };
   const int wm = wave & 1, wn = wave >> 1;
   f32x16 acc[2][2];
@@ -95,26 +102,26 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const uint8_t 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-  uint4 qa, qb;
-  float da, db;
+  uint4 qa;
+  float da;
+  u32x4 xb[4];
   ldW(0, qa, da);
-  ldX(0, qb, db);
+  ldX(0, xb);
   const int r = lane & 31, h = lane >> 5;
   for (int kb = 0; kb < nb; kb += 2) {
     // dequantize this step's units into LDS
-    half8 ha[4], hb[4];
+    half8 ha[4];
     deq_block_f16(qa, da, ha);
-    deq_block_f16(qb, db, hb);
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       *(half8 *)&As[u * GM_LD + ub * 32 + 8 * w] = ha[w];
-      *(half8 *)&Bs[u * GM_LD + ub * 32 + 8 * w] = hb[w];
+      *(u32x4 *)&Bs[u * GM_LD + ub * 32 + 8 * w] = xb[w];
     }
     __syncthreads();
     // next step's units in flight during the MFMAs
     if (kb + 2 < nb) {
       ldW(kb + 2, qa, da);
-      ldX(kb + 2, qb, db);
+      ldX(kb + 2, xb);
     }
 #pragma unroll
     for (int kk = 0; kk < GM_BK / 16; ++kk) {
@@ -167,9 +174,13 @@ int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, fl
   const size_t nbk = (size_t)n * (W.k / QK);
   const uint8_t *xqs = (const uint8_t *)xq;
   const float *xdd = (const float *)(xqs + nbk * 16);
+  _Float16 *x16 = nullptr;
+  VSIM_HIP(hipMallocAsync((void **)&x16, nbk * QK * sizeof(_Float16), s));
+  hipLaunchKernelGGL(k_act_deq_f16, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, xqs, xdd, nbk, (half8 *)x16);
   const dim3 grid((W.rows + GM_BM - 1) / GM_BM, (n + GM_BN - 1) / GM_BN);
-  hipLaunchKernelGGL(k_gemm_q4_f16, grid, dim3(GM_THREADS), 0, s, W, xqs, xdd, n, bias, y);
+  hipLaunchKernelGGL(k_gemm_q4_f16, grid, dim3(GM_THREADS), 0, s, W, x16, n, bias, y);
   VSIM_HIP(hipGetLastError());
+  VSIM_HIP(hipFreeAsync(x16, s));
   return VSIM_OK;
 }
 

@@ -99,6 +99,8 @@ struct vsim_model {
   // fast-mode decode step (fast_decode.hip): fc_out split-K partial rows and attention
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
   float *fast_ffp = nullptr, *fast_part = nullptr;
+  void *pf_scratch = nullptr;  // fast prefill: fp16 K / V^T copies (attn_prefill.hip)
+  size_t pf_bytes = 0;
 
   // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
   // fc_out, whose K = 4E chain is the layer's critical path
@@ -141,6 +143,9 @@ void free_scratch(vsim_model *m) {
   if (m->hist_dev) (void)hipFree(m->hist_dev);
   if (m->tail_done) (void)hipFree(m->tail_done);
   m->tail_done = nullptr;
+  if (m->pf_scratch) (void)hipFree(m->pf_scratch);
+  m->pf_scratch = nullptr;
+  m->pf_bytes = 0;
   if (m->fast_ffp) (void)hipFree(m->fast_ffp);
   if (m->fast_part) (void)hipFree(m->fast_part);
   m->fast_ffp = m->fast_part = nullptr;
@@ -480,7 +485,12 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
   if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
     // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
-    RC(launch_attn_prefill_f16(m->Qb, kc, vc, d, H, N, n_past, scale, m->attn_in, s)); ++nk;
+    if (!m->pf_scratch) {  // (prompt evals are never graph-captured: allocating here is safe)
+      m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
+      VSIM_HIP(hipMalloc(&m->pf_scratch, m->pf_bytes));
+    }
+    RC(launch_attn_prefill_f16(m->Qb, kc, vc, d, H, N, n_past, scale, m->attn_in, s, m->pf_scratch, m->pf_bytes));
+    nk += 2;
   } else {
     RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
     RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
