@@ -148,7 +148,7 @@ def fast_companion(model, n_past, tok, steps):
     gbs = q4_weight_bytes(arch_s, hp) * steps / dt / 1e9
     return {"value": round(steps / dt, 3), "unit": "tokens/s", "steps": steps,
             "weight_stream_GBps": round(gbs, 1), "frac_of_peak": round(gbs / PEAK_HBM_GBS, 4),
-            "kernels": "k_fast_ln, k_fast_gemv, k_fast_tail, k_fast_oproj_join (fast_decode.hip)",
+            "kernels": "k_fast_gemv (LayerNorm prologue), k_fast_tail, k_fast_oproj_join (fast_decode.hip)",
             "traffic_per_gemv_launch": (round(pmc_traffic_per_launch(mode="fast"))
                                         if pmc_traffic_per_launch(mode="fast") else None),
             "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": agree / len(rel),

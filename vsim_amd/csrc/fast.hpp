@@ -49,6 +49,11 @@ struct FastGemv {
   const int *npast;
   const double2 *cs;                // [n_ctx][n_rot/2]
   int d, n_rot, style;
+  // LayerNorm in the prologue (lnx non-null): every workgroup normalizes the residual row
+  // lnx with the affine of its job's `act` and quantizes it into LDS, while its first weight
+  // batch is in flight; xq/xd are then unused
+  const float *lnx;
+  const float *lnw[2], *lnb[2];
 };
 
 struct FastTail {

@@ -97,26 +97,27 @@ __device__ __forceinline__ int dot_q4(uint4 q, uint4 x) {
 }
 
 // One wave's share of a 32-row tile: blocks b = b0 + h + 2i < b1 (h = lane >> 5, row =
-// lane & 31), FD_U loads per lane in flight, the next batch issued before the current one
+// lane & 31), U loads per lane in flight, the next batch issued before the current one
 // is consumed.  The activation (nibbles + scales) is read from LDS.  `pre` tells whether
 // batch 0 was already issued by the caller (into qa/da).
+template <int U = FD_U>
 struct TileStream {
   const uint8_t *qs;  // tile's nibble plane: block b row r at (b*32 + r)*16
   const float *dd;    // tile's scale plane: (b*32 + r)
   int b0, b1, lane;
   int xoff = 0;  // first block of the activation slice staged in LDS
-  uint4 qa[FD_U];
-  float da[FD_U];
+  uint4 qa[U];
+  float da[U];
 
   // Slots past the wave's range still load (a neighbour's blocks, or the arena's FD_PAD
   // slack past the last tensor) and get a zero scale: constant offsets, no per-slot branch.
   __device__ __forceinline__ void load(uint4 *q, float *dw, int it) {
     const int r = lane & 31, h = lane >> 5;
-    const int bs = b0 + h + 2 * it * FD_U;
+    const int bs = b0 + h + 2 * it * U;
     const uint8_t *qp = qs + ((size_t)bs * T32 + r) * 16;  // slot u at + u * 1 KB
     const float *dp = dd + (size_t)bs * T32 + r;           // slot u at + u * 64 floats
 #pragma unroll
-    for (int u = 0; u < FD_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(qp + u * 2 * T32 * 16));
       q[u] = make_uint4(v.x, v.y, v.z, v.w);
       dw[u] = __builtin_nontemporal_load(dp + u * 2 * T32);  // zeroed past b1 in consume
@@ -127,8 +128,8 @@ struct TileStream {
                                            const float *xd, float acc) {
     const int h = lane >> 5;
 #pragma unroll
-    for (int u = 0; u < FD_U; ++u) {
-      const int bu = b0 + h + 2 * (it * FD_U + u);
+    for (int u = 0; u < U; ++u) {
+      const int bu = b0 + h + 2 * (it * U + u);
       const int b = min(bu, b1 - 1) - xoff;  // activation slot in LDS
       const uint4 x = xq[b];
       int s = __builtin_amdgcn_sdot8((int)(q[u].x ^ 0x88888888u), (int)x.x, 0, false);
@@ -139,7 +140,7 @@ struct TileStream {
     }
     return acc;
   }
-  __device__ __forceinline__ int iters() const { return (b1 - b0 + 2 * FD_U - 1) / (2 * FD_U); }
+  __device__ __forceinline__ int iters() const { return (b1 - b0 + 2 * U - 1) / (2 * U); }
   __device__ __forceinline__ void prefetch() { load(qa, da, 0); }
   // runs all batches; batch 0 must have been prefetched.  One register set: with 8 waves
   // per workgroup a K = 4096 tile is one batch per wave, and the other resident workgroups
@@ -264,28 +265,92 @@ __global__ void __launch_bounds__(LN_NT) k_fast_ln(FastLn P) {
   }
 }
 
+// The LayerNorm of k_fast_ln in a GEMV workgroup's prologue: the residual row and the
+// affine are loaded (PER float4 of each per thread) before the workgroup's first weight
+// batch, the moments reduced while that batch is in flight, and the normalized row
+// quantized straight into the LDS activation slots (8 lanes per 32-value block, fq_oct).
+template <int NT, int PER>
+struct LnStage {
+  f32x4 x[PER], w[PER], b[PER];
+  __device__ __forceinline__ void load(const float *lx, const float *lw, const float *lb, int E) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      int e = 4 * ((int)threadIdx.x + NT * k);
+      e = e < E ? e : 0;  // (the tail's elements are masked in finish)
+      x[k] = *(const f32x4 *)(lx + e);
+      w[k] = *(const f32x4 *)(lw + e);
+      b[k] = *(const f32x4 *)(lb + e);
+    }
+  }
+  __device__ __forceinline__ void finish(int E, uint4 *xq, float *xd, double *red) {
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    double s = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const f32x4 v = 4 * (tid + NT * k) < E ? x[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      s += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+      s2 += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+    }
+    s = wave_sum_d(s);
+    s2 = wave_sum_d(s2);
+    if (lane == 0) {
+      red[2 * wid] = s;
+      red[2 * wid + 1] = s2;
+    }
+    __syncthreads();
+    s = 0.0;
+    s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
+      s += red[2 * k];
+      s2 += red[2 * k + 1];
+    }
+    const double mean = s / E;
+    const double var = s2 / E - mean * mean;
+    const float scale = (float)(1.0 / sqrt(var + (double)1e-5f));
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int f = tid + NT * k;  // float4 index; lanes 8g..8g+7 hold block f / 8
+      const bool ok = 4 * f < E;   // uniform over the 8 lanes (E % 32 == 0)
+      float4 y;
+      y.x = w[k].x * ((float)((double)x[k].x - mean) * scale) + b[k].x;
+      y.y = w[k].y * ((float)((double)x[k].y - mean) * scale) + b[k].y;
+      y.z = w[k].z * ((float)((double)x[k].z - mean) * scale) + b[k].z;
+      y.w = w[k].w * ((float)((double)x[k].w - mean) * scale) + b[k].w;
+      const int blk = ok ? f >> 3 : 0;
+      fq_oct(y, lane, ok, (uint8_t *)&xq[blk], &xd[blk], (uint16_t)0x8888);
+    }
+  }
+};
+
 // ------------------------------------------------------------------ GEMV batch (K1, head)
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 6) k_fast_gemv(FastGemv P) {
+// LNP = 0: activations staged from global Q4 rows; LNP > 0: LayerNorm prologue (LnStage
+// with LNP float4 per thread).
+template <int NW, int LNP>
+__global__ void __launch_bounds__(64 * NW, LNP > 2 ? 5 : 6) k_fast_gemv(FastGemv P) {
   __shared__ uint4 xq[FD_MAXE / QK];
   __shared__ float xd[FD_MAXE / QK];
   __shared__ float part[2 * NW][T32];
+  __shared__ double red[2 * NW];
   int t = blockIdx.x, ji = 0;
   while (ji + 1 < P.nj && t >= P.j[ji].w.tiles) { t -= P.j[ji].w.tiles; ++ji; }
   const FastJob &J = P.j[ji];
   const int nb = J.w.nb();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  TileStream ts;
+  TileStream<> ts;
   ts.qs = J.w.qs + (size_t)t * nb * T32 * 16;
   ts.dd = J.w.d + (size_t)t * nb * T32;
   ts.b0 = wave * nb / NW;
   ts.b1 = (wave + 1) * nb / NW;
   ts.lane = lane;
   ActStage st;
-  st.load(P.xq[J.act], P.xd[J.act], 0, nb);
+  LnStage<64 * NW, LNP> ln;
+  if constexpr (LNP > 0) ln.load(P.lnx, P.lnw[J.act], P.lnb[J.act], nb * QK);
+  else st.load(P.xq[J.act], P.xd[J.act], 0, nb);
   const int n_past = J.epi >= FE_ROPE_Q ? *P.npast : 0;
   ts.prefetch();
-  st.store(nb, xq, xd);
+  if constexpr (LNP > 0) ln.finish(nb * QK, xq, xd, red);
+  else st.store(nb, xq, xd);
   __syncthreads();
   const float acc = ts.run(xq, xd);
   const float s = tile_reduce<NW>(acc, part);
@@ -329,6 +394,12 @@ __global__ void __launch_bounds__(64 * NW, 6) k_fast_gemv(FastGemv P) {
 
 // ------------------------------------------------------------------ K2: fc_out | attention
 constexpr int FT_NT = 64 * FD_WAVES;
+// fc_out's stream: K / sf blocks per tile over 8 waves, several batches per wave, and only
+// H * nchunk + tiles * sf workgroups (about 1.5 per CU for GPT-J): more loads in flight per
+// lane than K1 (which has 3 workgroups on every CU)
+// (A/B on GPT-J, 64 tokens: U = 4 at 4 workgroups per CU 973 tok/s, U = 8 923)
+constexpr int FT_U = 4;
+constexpr int FT_OCC = 4;
 
 // One (head, chunk) of flash-decoding attention.  Wave w takes positions p0 + 8w .. +7 of
 // the chunk: its K and V rows and q are loaded at once (one round trip), one float4 of the
@@ -412,7 +483,10 @@ __device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
   }
 }
 
-__global__ void __launch_bounds__(FT_NT, 6) k_fast_tail(FastTail A) {
+__device__ __forceinline__ void fast_fcout_part(const FastTail &A, int idx, uint4 *xq, float *xd,
+                                                float (*part)[T32]);
+
+__global__ void __launch_bounds__(FT_NT, FT_OCC) k_fast_tail(FastTail A) {
   __shared__ uint4 xq[FD_MAXE / QK];
   __shared__ float xd[FD_MAXE / QK];
   __shared__ float part[2 * FD_WAVES][T32];
@@ -422,12 +496,17 @@ __global__ void __launch_bounds__(FT_NT, 6) k_fast_tail(FastTail A) {
     fast_attn_chunk(A, blockIdx.x / A.nchunk, blockIdx.x % A.nchunk, ored);
     return;
   }
-  const int idx = blockIdx.x - na;
+  fast_fcout_part(A, blockIdx.x - na, xq, xd, part);
+}
+
+// One (tile, K split) of fc_out: partial rows into ffp[split].
+__device__ __forceinline__ void fast_fcout_part(const FastTail &A, int idx, uint4 *xq, float *xd,
+                                                float (*part)[T32]) {
   const int t = idx / A.sf, sp = idx % A.sf;
   const int nb = A.wf.nb();
   const int kb0 = sp * nb / A.sf, kb1 = (sp + 1) * nb / A.sf;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  TileStream ts;
+  TileStream<FT_U> ts;
   ts.qs = A.wf.qs + (size_t)t * nb * T32 * 16;
   ts.dd = A.wf.d + (size_t)t * nb * T32;
   ts.b0 = kb0 + wave * (kb1 - kb0) / FD_WAVES;
@@ -501,25 +580,23 @@ __device__ __forceinline__ void attn_merge_lds(const FastOproj &P, int E, uint4 
   }
 }
 
-__global__ void __launch_bounds__(64 * FD_OWAVES) k_fast_oproj_join(FastOproj P) {
-  constexpr int NT = 64 * FD_OWAVES;
-  __shared__ uint4 xq[FD_MAXE / QK];
-  __shared__ float xd[FD_MAXE / QK];
-  __shared__ float part[2 * FD_OWAVES][T32];
-  __shared__ float wgt[FD_MAXW];
-  const int t = blockIdx.x, nb = P.w.nb(), E = P.w.rows;
+// Out-projection tile t and the residual join (K3).
+template <int NW>
+__device__ __forceinline__ void fast_oproj_tile(const FastOproj &P, int t, uint4 *xq, float *xd, float (*part)[T32],
+                                                float *wgt) {
+  const int nb = P.w.nb(), E = P.w.rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  TileStream ts;
+  TileStream<> ts;
   ts.qs = P.w.qs + (size_t)t * nb * T32 * 16;
   ts.dd = P.w.d + (size_t)t * nb * T32;
-  ts.b0 = wave * nb / FD_OWAVES;
-  ts.b1 = (wave + 1) * nb / FD_OWAVES;
+  ts.b0 = wave * nb / NW;
+  ts.b1 = (wave + 1) * nb / NW;
   ts.lane = lane;
   ts.prefetch();
-  attn_merge_lds<NT>(P, E, xq, xd, wgt);
+  attn_merge_lds<64 * NW>(P, E, xq, xd, wgt);
   __syncthreads();
   const float acc = ts.run(xq, xd);
-  const float s = tile_reduce<FD_OWAVES>(acc, part);
+  const float s = tile_reduce<NW>(acc, part);
   if (wave == 0 && lane < T32) {
     const int row = t * T32 + lane;
     float f = 0.0f;
@@ -527,6 +604,14 @@ __global__ void __launch_bounds__(64 * FD_OWAVES) k_fast_oproj_join(FastOproj P)
     const float attn = P.bo ? s + P.bo[row] : s;
     P.out[row] = P.x[row] + (attn + (f + P.bproj[row]));
   }
+}
+
+__global__ void __launch_bounds__(64 * FD_OWAVES) k_fast_oproj_join(FastOproj P) {
+  __shared__ uint4 xq[FD_MAXE / QK];
+  __shared__ float xd[FD_MAXE / QK];
+  __shared__ float part[2 * FD_OWAVES][T32];
+  __shared__ float wgt[FD_MAXW];
+  fast_oproj_tile<FD_OWAVES>(P, blockIdx.x, xq, xd, part, wgt);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -549,7 +634,17 @@ int launch_fast_gemv(const FastGemv &P, int E, hipStream_t s) {
     }
     tiles += P.j[i].w.tiles;
   }
-  hipLaunchKernelGGL(k_fast_gemv<FD_WAVES>, dim3(tiles), dim3(64 * FD_WAVES), 0, s, P);
+  const dim3 g(tiles), b(64 * FD_WAVES);
+  if (!P.lnx) {
+    hipLaunchKernelGGL((k_fast_gemv<FD_WAVES, 0>), g, b, 0, s, P);
+  } else {
+    switch ((E / 4 + 64 * FD_WAVES - 1) / (64 * FD_WAVES)) {  // float4 per thread
+      case 1: hipLaunchKernelGGL((k_fast_gemv<FD_WAVES, 1>), g, b, 0, s, P); break;
+      case 2: hipLaunchKernelGGL((k_fast_gemv<FD_WAVES, 2>), g, b, 0, s, P); break;
+      case 3: hipLaunchKernelGGL((k_fast_gemv<FD_WAVES, 3>), g, b, 0, s, P); break;
+      default: hipLaunchKernelGGL((k_fast_gemv<FD_WAVES, 4>), g, b, 0, s, P); break;
+    }
+  }
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

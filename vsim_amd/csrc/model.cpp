@@ -562,6 +562,14 @@ int fast_sf(const vsim_model *m) {
   return sf;
 }
 
+bool fast_ln_fused() {
+  static const bool v = [] {
+    const char *e = getenv("VSIM_FAST_LN");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 bool fast_decode_ok(const vsim_model *m) {
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H;
   const int nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
@@ -590,23 +598,32 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
   for (int il = m->l0; il < m->l1; ++il) {
     const LayerW &L = m->layers[il - m->l0];
     const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
-    // LayerNorm(s) -> Q4 activations (GPT-J: one LayerNorm feeds attention and MLP)
-    FastLn N{};
-    N.x = R[cur];
-    N.E = E;
-    N.n = gptj ? 1 : 2;
-    N.w[0] = L.ln1_w;
-    N.b[0] = L.ln1_b;
-    N.w[1] = L.ln2_w;
-    N.b[1] = L.ln2_b;
-    N.qs[0] = q1;
-    N.d[0] = d1;
-    N.qs[1] = q2;
-    N.d[1] = d2;
-    RC(launch_fast_ln(N, s));
-    ++nk;
-    // {fc_in -> GELU -> quantize, Q, K, V}
+    // LayerNorm(s) -> Q4 activations (GPT-J: one LayerNorm feeds attention and MLP): in
+    // the GEMV's prologue (VSIM_FAST_LN=0: a separate k_fast_ln launch)
     FastGemv P{};
+    if (fast_ln_fused()) {
+      P.lnx = R[cur];
+      P.lnw[0] = L.ln1_w;
+      P.lnb[0] = L.ln1_b;
+      P.lnw[1] = gptj ? L.ln1_w : L.ln2_w;
+      P.lnb[1] = gptj ? L.ln1_b : L.ln2_b;
+    } else {
+      FastLn N{};
+      N.x = R[cur];
+      N.E = E;
+      N.n = gptj ? 1 : 2;
+      N.w[0] = L.ln1_w;
+      N.b[0] = L.ln1_b;
+      N.w[1] = L.ln2_w;
+      N.b[1] = L.ln2_b;
+      N.qs[0] = q1;
+      N.d[0] = d1;
+      N.qs[1] = q2;
+      N.d[1] = d2;
+      RC(launch_fast_ln(N, s));
+      ++nk;
+    }
+    // {fc_in -> GELU -> quantize, Q, K, V}
     P.xq[0] = q1;
     P.xd[0] = d1;
     P.xq[1] = gptj ? q1 : q2;
@@ -644,10 +661,6 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     T.nchunk = nchunk;
     T.scale = scale;
     T.part = m->fast_part;
-    ev = prof_begin(m);
-    RC(launch_fast_tail(T, s));
-    prof_end(m, ev, w4_algo_bytes(T.wf));
-    ++nk;
     // attention merge + out-projection + residual join into the other buffer
     FastOproj O{};
     O.w = w4_view(L.wo, E, E);
@@ -662,23 +675,33 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     O.x = R[cur];
     O.out = R[cur ^ 1];
     ev = prof_begin(m);
+    RC(launch_fast_tail(T, s));
+    prof_end(m, ev, w4_algo_bytes(T.wf));
+    ++nk;
+    ev = prof_begin(m);
     RC(launch_fast_oproj_join(O, s));
     prof_end(m, ev, w4_algo_bytes(O.w));
     ++nk;
     cur ^= 1;
   }
   if (m->last) {
-    FastLn N{};
-    N.x = R[cur];
-    N.E = E;
-    N.n = 1;
-    N.w[0] = m->lnf_w;
-    N.b[0] = m->lnf_b;
-    N.qs[0] = q1;
-    N.d[0] = d1;
-    RC(launch_fast_ln(N, s));
-    ++nk;
     FastGemv P{};
+    if (fast_ln_fused()) {
+      P.lnx = R[cur];
+      P.lnw[0] = P.lnw[1] = m->lnf_w;
+      P.lnb[0] = P.lnb[1] = m->lnf_b;
+    } else {
+      FastLn N{};
+      N.x = R[cur];
+      N.E = E;
+      N.n = 1;
+      N.w[0] = m->lnf_w;
+      N.b[0] = m->lnf_b;
+      N.qs[0] = q1;
+      N.d[0] = d1;
+      RC(launch_fast_ln(N, s));
+      ++nk;
+    }
     P.xq[0] = P.xq[1] = q1;
     P.xd[0] = P.xd[1] = d1;
     P.nj = 1;

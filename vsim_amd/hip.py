@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libvsim_hip.so")
+LIB_PATH = os.environ.get("VSIM_LIB") or os.path.join(HERE, "_build", "libvsim_hip.so")  # VSIM_LIB: A/B builds
 
 MODE_EXACT = 0
 MODE_FAST = 1
