@@ -26,7 +26,7 @@ constexpr int ATT_DPL = 4;      // max float4 of the head dimension per lane in 
 // and softmax (identical in each), then the KQV chains and quantization of output columns
 // [part*c, part*c + c), c = d / S, so a head's V rows spread over S CUs.  Every part writes
 // the same new K/V cache row (identical bytes) before reading it back.
-template <int NT>
+template <int NT, bool CO = false>
 __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, unsigned long long *prof = nullptr) {
   constexpr int ATT_THREADS = NT, ATT_WAVES = NT / 64;
   const int S = A.nsplit > 1 ? A.nsplit : 1, h = hs / S, part = hs % S;
@@ -207,13 +207,13 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, u
 #define ATT_STEP
 #undef ATT_STEP
 #undef ATT_TLOAD
-    if (tid < c && A.out) A.out[h * d + c0 + tid] = y;
+    if (tid < c && A.out) st_out<CO>(A.out + h * d + c0 + tid, y);
   }
   // quantize the part's outputs: wave w holds columns c0 + 64w .. +63, two 32-blocks
   if (wid * 64 < c) {
     const int blk = (h * d + c0 + wid * 64) / QK + (lane >> 5);
     const bool ok = wid * 64 + (lane & ~31) < c;
-    quantize_half(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
+    quantize_half<CO>(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
   }
   if (prof && h == 0 && tid == 0) prof[4] = __builtin_amdgcn_s_memtime();
 }

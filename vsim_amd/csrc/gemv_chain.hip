@@ -733,13 +733,14 @@ struct SoloShape {
 constexpr int C5_RING = 3;
 
 // PF: prefetch distance of the weight loads in chunks (register ring of PF+1 sets)
-template <int DBG, int CB, int PF>
-__global__ void __launch_bounds__(64 * SoloShape<CB>::WAVES, 1) k_gemv_solo(GemvBatch B) {
+// One 64-row group g of batch B (groups numbered job by job); P: the pair-term ring.
+// Every wave returns from here (producers and fillers early); all take nit barriers.
+template <int DBG, int CB, int PF, bool CO = false>
+__device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[64 * SoloShape<CB>::LD]) {
   using S = SoloShape<CB>;
-  __shared__ __attribute__((aligned(16))) float P[C5_RING][64 * S::LD];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  int g = blockIdx.x, ji = 0;
+  int ji = 0;
   while (ji < B.nj) {
     const int ng = (B.j[ji].w.tiles + 1) / 2;
     if (g < ng) break;
@@ -903,14 +904,209 @@ __global__ void __launch_bounds__(64 * SoloShape<CB>::WAVES, 1) k_gemv_solo(Gemv
     float gv = 0.0f;
     if (ok) {
       gv = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
-      if (y) y[row] = gv;
+      if (y) st_out<CO>(y + row, gv);
     }
     const int blk = row / QK;
-    quantize_half(gv, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
+    quantize_half<CO>(gv, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
                   B.j[ji].oxd + (size_t)blk * QK);
   } else if (row < rows) {
-    y[row] = bias ? acc + bias[row] : acc;
+    st_out<CO>(y + row, bias ? acc + bias[row] : acc);
   }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int DBG, int CB, int PF>
+__global__ void __launch_bounds__(64 * SoloShape<CB>::WAVES, 1) k_gemv_solo(GemvBatch B) {
+  __shared__ __attribute__((aligned(16))) float P[C5_RING][64 * SoloShape<CB>::LD];
+  // (timing experiments: DBG 16 / 32 raise the kernel's VGPR count to 144 / 104)
+  if (DBG & 16) asm volatile("v_mov_b32 v143, 0" ::: "v143");
+  if (DBG & 32) asm volatile("v_mov_b32 v103, 0" ::: "v103");
+  solo_body<DBG & 15, CB, PF>(B, blockIdx.x, P);
+}
+
+// ================================================================== one launch per layer
+// An exact decode layer in one grid, so that fc_out's K = 4E chain (the layer's longest
+// dependency) starts as soon as fc_in's chains end and the attention branch fills the CUs
+// beside it.  Segments in grid order:
+//   ln  (join of the previous layer +) LayerNorm(s) + quantize, 8 workgroups per norm
+//                                                                   -> counts cnt[192]
+//   in  fc_in (+ bias, GELU, requantize), 64-row solo groups: wait cnt[192] == n_ln
+//                                                                   -> counts cnt[0]
+//   f   fc_out: waits cnt[0] == n_in; solo groups or 32-row tiles
+//   q   Q, K, V, 64-row solo groups: wait cnt[192] == n_ln          -> counts cnt[64]
+//   a   attention heads: wait cnt[64] == n_q                        -> count cnt[128]
+//   o   out-projection, 32-row tiles: waits cnt[128] == n_a
+// (qfirst: q before f; n_ln == 0: the LayerNorm ran as its own launch.)  A segment waits
+// only on lower-indexed workgroups, which the dispatcher has placed before it, so every
+// wait ends.  The counters are zeroed before the launch (a memset node per token).  Segments of 32-row tiles and heads use
+// the first C2_THREADS threads; the other waves leave at once (s_barrier then counts only
+// the waves still running).  A producer segment releases its stores at agent scope before
+// it counts; a waiting one acquires after its wait.  The activation factors read by a
+// waiting solo segment's scalar loads were written in this launch, but no workgroup reads
+// them before its wait, so the scalar cache holds no stale copy.
+extern unsigned *g_norm_stats;
+constexpr int LX_CB = 6, LX_PF = 3;
+constexpr int LX_THREADS = 64 * SoloShape<LX_CB>::WAVES;
+static_assert(LX_THREADS >= C2_THREADS, "tile segments run on the first C2_THREADS threads");
+struct LayerExactJob {
+  GemvBatch in, f, q, o;
+  AttnJob a;
+  LnQuantJob ln[2];  // the layer's LayerNorm(s) (+ the previous layer's join), n_ln > 0
+  unsigned *stats;   // LayerNorm fallback counters (g_norm_stats)
+  unsigned *cnt;
+  int n_ln, ln_n, n_in, n_f, n_q, n_a, fsolo, qfirst;
+  int dbg;  // VSIM_LX_DBG (timing experiments): skip the work of in 1, f 2, q 4, a 8, o 16
+};
+union LxLds {
+  float s[C5_RING][64 * SoloShape<LX_CB>::LD];
+  C2Lds g;
+};
+
+// Hand-offs (cdna_hip_programming.md §6 Guideline 16, counter form): producers store their
+// outputs sc1 (st_out<true>), every wave drains its stores, one lane adds to the counter; a
+// consumer polls relaxed in one lane, then ONE agent acquire (this CU's L1) before the barrier.
+// (A release fence per producer workgroup, i.e. an L2 write-back each, made this launch 2x
+// slower than the three-launch layer.)  Consumer loads of handed-off bytes: vector loads
+// behind the acquire, and fc_out's scalar factor loads, which no workgroup issues before
+// its wait in this launch (the scalar cache starts the launch empty).
+// acq = false: the segment reads the handed-off bytes only by scalar loads (the solo
+// producers' activation factors), which the L1 acquire does not concern.
+__device__ __forceinline__ void lx_wait(const unsigned *c, unsigned target, bool acq = true) {
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0)
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(4);
+    if (acq) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void lx_count(unsigned *c) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 output stores
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(LX_THREADS, 1) k_layer_exact(LayerExactJob T) {
+  __shared__ __attribute__((aligned(16))) LxLds L;
+  const int wave = threadIdx.x >> 6;
+  int b = blockIdx.x;
+  if (b < T.n_ln) {  // k_ln_quant's body (layer.hip), outputs stored sc1
+    const int part = b % 8;
+    const LnQuantJob &J = T.ln[b / 8];
+    const int n = T.ln_n, nb = n / QK, lane = threadIdx.x & 63;
+    const int b0 = part * nb / 8, b1 = (part + 1) * nb / 8;
+    float *row = (float *)&L;
+    ln_exact_lds_t<LX_THREADS>(J.x, row, n, J.w, J.b, part == 0 ? T.stats : nullptr, J.ja, J.jab, J.jf, J.jfb,
+                               J.jout, nullptr, b0 * QK / 4, b1 * QK / 4);
+    for (int b2 = wave; b0 + 2 * b2 < b1; b2 += LX_THREADS / 64) {
+      const int bb = b0 + 2 * b2 + (lane >> 5);
+      const bool ok = bb < b1;
+      const float v = ok ? row[bb * QK + (lane & 31)] : 0.0f;
+      quantize_half<true>(v, lane, ok, J.qs + (size_t)bb * 16, J.d + bb, J.xd + (size_t)bb * QK);
+    }
+    lx_count(T.cnt + 192);
+    return;
+  }
+  b -= T.n_ln;
+  if (b < T.n_in) {
+    if (T.n_ln) lx_wait(T.cnt + 192, (unsigned)T.n_ln, false);
+    if (!(T.dbg & 1)) solo_body<0, LX_CB, LX_PF, true>(T.in, b, L.s);
+    lx_count(T.cnt);
+    return;
+  }
+  b -= T.n_in;
+  const int nf = T.n_f, nq = T.n_q;
+  const bool is_f = T.qfirst ? (b >= nq && b < nq + nf) : b < nf;
+  const bool is_q = T.qfirst ? b < nq : (b >= nf && b < nf + nq);
+  if (is_f) {
+    b -= T.qfirst ? nq : 0;
+    if (T.n_in > 0) lx_wait(T.cnt, (unsigned)T.n_in, !T.fsolo);
+    if (T.dbg & 2) {
+    } else if (T.fsolo) {
+      solo_body<0, LX_CB, LX_PF>(T.f, b, L.s);
+    } else if (wave < C2_THREADS / 64) {
+      chain32_body<0>(T.f, b, L.g);
+    }
+    return;
+  }
+  if (is_q) {
+    b -= T.qfirst ? 0 : nf;
+    if (T.n_ln) lx_wait(T.cnt + 192, (unsigned)T.n_ln, false);
+    if (!(T.dbg & 4)) solo_body<0, LX_CB, LX_PF, true>(T.q, b, L.s);
+    lx_count(T.cnt + 64);
+    return;
+  }
+  b -= nf + nq;
+  if (wave >= C2_THREADS / 64) return;
+  if (b < T.n_a) {
+    lx_wait(T.cnt + 64, (unsigned)nq);
+    if (!(T.dbg & 8)) attn_body<C2_THREADS, true>(T.a, b, (float *)&L);
+    lx_count(T.cnt + 128);
+    return;
+  }
+  b -= T.n_a;
+  lx_wait(T.cnt + 128, (unsigned)T.n_a);
+  if (!(T.dbg & 16)) chain32_body<0>(T.o, b, L.g);
+}
+
+static int solo_groups(const GemvBatch &B) {
+  int g = 0;
+  for (int i = 0; i < B.nj; ++i) g += (B.j[i].w.tiles + 1) / 2;
+  return g;
+}
+static int batch_tiles(const GemvBatch &B) {
+  int t = 0;
+  for (int i = 0; i < B.nj; ++i) t += B.j[i].w.tiles;
+  return t;
+}
+
+int launch_layer_exact(const LnQuantJob *ln, int n_ln, const GemvBatch &in, const GemvBatch &f, const GemvBatch &q,
+                       const GemvBatch &o, const AttnJob &a, unsigned *cnt, int n_ctx, int fsolo, int qfirst,
+                       hipStream_t s) {
+  const int S = a.nsplit > 1 ? a.nsplit : 1;
+  if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
+      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(LxLds)) {
+    set_error("layer kernel: attention shape (head dim, n_ctx) outside the fused kernel's range");
+    return VSIM_EINVAL;
+  }
+  for (const GemvBatch *B : {&in, &f, &q, &o})
+    for (int i = 0; i < B->nj; ++i)
+      if (B->j[i].w.k % QK != 0 || B->j[i].w.k <= 0 || !B->j[i].xd) {
+        set_error("layer kernel: K must be a positive multiple of 32 and the activation factors set");
+        return VSIM_EINVAL;
+      }
+  LayerExactJob T;
+  T.n_ln = 8 * n_ln;
+  T.ln_n = n_ln ? in.j[0].w.k : 0;
+  for (int i = 0; i < 2; ++i) T.ln[i] = n_ln ? ln[i < n_ln ? i : 0] : LnQuantJob{};
+  T.stats = g_norm_stats;
+  if (n_ln && (in.nj != 1 || (size_t)T.ln_n * sizeof(float) > sizeof(LxLds) || T.ln_n % QK != 0)) {
+    set_error("layer kernel: the LayerNorm segment needs fc_in in the launch and E within the LDS row");
+    return VSIM_EINVAL;
+  }
+  T.in = in;
+  T.f = f;
+  T.q = q;
+  T.o = o;
+  T.a = a;
+  T.cnt = cnt;
+  T.n_in = solo_groups(in);
+  T.n_f = fsolo ? solo_groups(f) : batch_tiles(f);
+  T.n_q = solo_groups(q);
+  T.n_a = a.H * S;
+  T.fsolo = fsolo;
+  T.qfirst = qfirst;
+  static const int dbg = [] {
+    const char *e = getenv("VSIM_LX_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  T.dbg = dbg;
+  const int grid = T.n_ln + T.n_in + T.n_f + T.n_q + T.n_a + batch_tiles(o);
+  hipLaunchKernelGGL(k_layer_exact, dim3(grid), dim3(LX_THREADS), 0, s, T);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
 }
 
 template <int DBG>
@@ -977,7 +1173,8 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
         C5L(0, 6, 5);
       } else {
         if (dbg == 1) C5L(1, 6, 3); else if (dbg == 2) C5L(2, 6, 3); else if (dbg == 4) C5L(4, 6, 3);
-        else if (dbg == 8) C5L(8, 6, 3); else if (dbg == 9) C5L(9, 6, 3); else C5L(0, 6, 3);
+        else if (dbg == 8) C5L(8, 6, 3); else if (dbg == 9) C5L(9, 6, 3);
+        else if (dbg == 16) C5L(16, 6, 3); else if (dbg == 32) C5L(32, 6, 3); else C5L(0, 6, 3);
       }
     }
 #undef C5L

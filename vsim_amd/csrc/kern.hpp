@@ -323,6 +323,17 @@ __device__ __forceinline__ void ln_exact_lds(const float *__restrict__ x, float 
 
 // Quantize one 32-value block per half-wave (lanes 0-31 -> block A, 32-63 -> block B) with
 // quantize_row_q4_0 semantics (see quantize_block_lanes below).
+// Stores of data that workgroups on other XCDs read later in the same launch (k_layer_exact):
+// agent-scope relaxed atomic stores are sc1 (write-through) stores, visible device-wide after
+// the storing wave's vmcnt drain, without the L2 write-back a release fence costs every
+// producer workgroup (MI355X_MICROARCH.md, inter-workgroup visibility).
+template <bool CO, typename T>
+__device__ __forceinline__ void st_out(T *p, T v) {
+  if constexpr (CO) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <bool CO = false>
 __device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
                                               float *xd_out) {
   // amax over the half-wave: DPP within rows of 16 lanes, then rows 0<->1 and 2<->3 by
@@ -346,9 +357,9 @@ __device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_
   word |= (uint32_t)dpp::mov<dpp::QP_XOR2, 0xF>((int)word, 0);
   word |= (uint32_t)dpp::mov<dpp::HALF_MIRROR, 0xF>((int)word, 0);
   if (ok) {
-    if ((l & 7) == 0) ((uint32_t *)qs_out)[l >> 3] = word;
-    if (l == 0) *d_out = d;
-    xd_out[xd_slot(l)] = d * (float)(q - 8);
+    if ((l & 7) == 0) st_out<CO>((uint32_t *)qs_out + (l >> 3), word);
+    if (l == 0) st_out<CO>(d_out, d);
+    st_out<CO>(xd_out + xd_slot(l), d * (float)(q - 8));
   }
 }
 

@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuant
   const int part = blockIdx.x % LNQ_SPLIT;
   const LnQuantJob &J = blockIdx.x < LNQ_SPLIT ? j0 : j1;
   unsigned long long *prof = PROF && blockIdx.x == 0 ? g_ln_prof : nullptr;
-  if (J.clear && blockIdx.x == 0 && threadIdx.x == 0) *J.clear = 0u;
+  if (J.clear && blockIdx.x == 0 && threadIdx.x < 3) J.clear[64 * threadIdx.x] = 0u;
   const int nb = n / QK, lane = threadIdx.x & 63;
   const int b0 = part * nb / LNQ_SPLIT, b1 = (part + 1) * nb / LNQ_SPLIT;  // this slice's blocks
   ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, part == 0 ? stats : nullptr, J.ja, J.jab, J.jf, J.jfb, J.jout,

@@ -212,8 +212,11 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMalloc((void **)&m->am_dev, sizeof(int)));
   VSIM_HIP(hipHostMalloc((void **)&m->am_host, sizeof(int), hipHostMallocDefault));
   VSIM_HIP(hipMalloc((void **)&m->hist_dev, (size_t)m->n_ctx * sizeof(int)));
-  VSIM_HIP(hipMalloc((void **)&m->tail_done, sizeof(unsigned)));
-  VSIM_HIP(hipMemset(m->tail_done, 0, sizeof(unsigned)));
+  // counters of the fused layer kernels at [0], [64], [128] (separate 256-byte lines)
+  // (k_layer_exact: one set per layer, [il - l0][256], zeroed by a memset node per token)
+  const size_t ncnt = (size_t)std::max(1, m->l1 - m->l0) * 256;
+  VSIM_HIP(hipMalloc((void **)&m->tail_done, ncnt * sizeof(unsigned)));
+  VSIM_HIP(hipMemset(m->tail_done, 0, ncnt * sizeof(unsigned)));
   {
     const size_t d = E / H, nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
     VSIM_HIP(fa(&m->fast_ffp, 8 * E));
@@ -562,6 +565,26 @@ int fast_sf(const vsim_model *m) {
   return sf;
 }
 
+static int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e && e[0] ? atoi(e) : dflt;
+}
+// VSIM_LAYER=1|2 select the one-launch layer kernel (k_layer_exact; 2: fc_in as a launch of
+// its own before it).  Bit-identical to the default three-launch layer, but not faster on
+// GPT-J-6B (489 vs 510 tok/s), so 0 is the default.
+int layer_mode() {
+  static const int v = env_int("VSIM_LAYER", 0);
+  return v;
+}
+int lx_fsolo() {  // VSIM_LX_FSOLO=0: fc_out as 32-row tiles inside k_layer_exact
+  static const int v = env_int("VSIM_LX_FSOLO", 1);
+  return v;
+}
+int lx_qfirst() {  // VSIM_LX_QFIRST=1: Q/K/V before fc_out in the grid
+  static const int v = env_int("VSIM_LX_QFIRST", 0);
+  return v;
+}
+
 bool fast_ln_fused() {
   static const bool v = [] {
     const char *e = getenv("VSIM_FAST_LN");
@@ -776,9 +799,20 @@ int enqueue_decode(vsim_model *m, int &nk) {
     }
     const bool tail = tail_env && !split && m->mode == VSIM_MODE_EXACT &&
                       (size_t)attn_lds_floats(d, m->n_ctx) * sizeof(float) <= 75264;
-    if (tail) j1.clear = m->tail_done;
-    RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
-    ++nk;
+    // VSIM_LAYER: 0 (default) the norm, {fc_in, Q, K, V}, then k_layer_tail; 1 the norm
+    // and everything after it in one launch (k_layer_exact); 2 the norm, fc_in, then the
+    // rest in one launch
+    const int lx = tail ? layer_mode() : 0;
+    unsigned *cnt = m->tail_done + (size_t)(lx ? il - m->l0 : 0) * 256;
+    if (lx && il == m->l0) {
+      VSIM_HIP(hipMemsetAsync(m->tail_done, 0, (size_t)(m->l1 - m->l0) * 256 * sizeof(unsigned), s));
+    }
+    const LnQuantJob lnj[2] = {j1, j2};
+    if (lx != 1) {
+      if (tail) j1.clear = m->tail_done;
+      RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
+      ++nk;
+    }
     if (pending) cur ^= 1;
     // 2. fc_in (+bias, GELU, requantize) -> 3. fc_out; beside it, on the second stream,
     //    Q/K/V -> attention -> out-projection.  fc_out's K = 4E chain (vsim.cpp:680-690) is
@@ -811,10 +845,15 @@ int enqueue_decode(vsim_model *m, int &nk) {
     job(BQ, q0 + 0, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
     job(BQ, q0 + 1, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
     job(BQ, q0 + 2, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
-    hipEvent_t *ev = prof_begin(m);
-    RC(launch_gemv_epi(B, m->mode, s));
-    prof_end(m, ev, split ? w4_algo_bytes(B.j[0].w) : w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
-    ++nk;
+    hipEvent_t *ev = nullptr;
+    if (lx != 1) {
+      GemvBatch Bi = B;
+      if (lx == 2) Bi.nj = 1;
+      ev = prof_begin(m);
+      RC(launch_gemv_epi(Bi, m->mode, s));
+      prof_end(m, ev, Bi.nj == 1 ? w4_algo_bytes(Bi.j[0].w) : w4_algo_bytes(Bi.j[0].w) + 3 * w4_algo_bytes(Bi.j[1].w));
+      ++nk;
+    }
     hipStream_t sa = s;  // attention branch
     if (split) {
       sa = m->stream2;
@@ -861,9 +900,22 @@ int enqueue_decode(vsim_model *m, int &nk) {
       job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
       Bo.nj = 1;
       job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
-      ev = prof_begin(m);
-      RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
-      prof_end(m, ev, w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w));
+      if (lx) {
+        GemvBatch Bi{}, Bq{};
+        Bi.nj = lx == 1 ? 1 : 0;
+        Bi.j[0] = B.j[0];
+        Bq.nj = 3;
+        for (int i = 0; i < 3; ++i) Bq.j[i] = B.j[1 + i];
+        ev = prof_begin(m);
+        RC(launch_layer_exact(lnj, lx == 1 ? (gptj ? 1 : 2) : 0, Bi, Bf, Bq, Bo, A, cnt, m->n_ctx, lx_fsolo(),
+                              lx_qfirst(), s));
+        prof_end(m, ev, (lx == 1 ? w4_algo_bytes(B.j[0].w) : 0) + 3 * w4_algo_bytes(B.j[1].w) +
+                            w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w));
+      } else {
+        ev = prof_begin(m);
+        RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
+        prof_end(m, ev, w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w));
+      }
       ++nk;
       pending = true;
       pend_ab = gptj ? nullptr : L.bo;
