@@ -112,6 +112,26 @@ def test_fast_mode_tracks_exact(tmp_path):
     assert cos > 0.95, cos
 
 
+@pytest.mark.parametrize("arch_name", ["small-gptj", "small-neox"])
+def test_fast_prefill_deterministic(arch_name, tmp_path):
+    """The fast prompt path (activations quantized straight to fp16, MFMA GEMM, MFMA
+    attention) gives the same logits bits on every run: fixed-order reductions only."""
+    arch_s, hp = mg.CONFIGS[arch_name]
+    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    path = str(tmp_path / "pfd.bin")
+    mg.write_model(path, arch_s, hp, seed=4, std=0.05)
+    ids = [(11 * i + 2) % hp.n_vocab for i in range(72)]
+    runs = []
+    for _ in range(2):
+        m = hip.Model.load(path, arch)
+        m.set_mode(hip.MODE_FAST)
+        a = m.eval(0, ids)
+        b = m.eval(len(ids), ids[:16])  # a second batch on top of the cache
+        runs.append(np.concatenate([a, b]))
+        m.close()
+    assert np.array_equal(runs[0].view(np.uint32), runs[1].view(np.uint32))
+
+
 def test_pipeline_stages_equal_single_stage(tmp_path):
     """Layer split: stage 0 = layers [0,1), stage 1 = [1,L) on one
     device, residual handed over in device memory — logits identical to one stage."""

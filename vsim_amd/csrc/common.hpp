@@ -245,6 +245,11 @@ int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, flo
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
 int launch_argmax(const float *x, int n, int *out, hipStream_t s);
 int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s);
+// fast-mode prompt batches (n >= GEMM_MIN_N): activation rows quantized (optionally after
+// bias + GELU) straight to the GEMM's fp16 operand x16 [n][K], and the GEMM on it
+constexpr int GEMM_MIN_N = 8;
+int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s);
+int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s);
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call)

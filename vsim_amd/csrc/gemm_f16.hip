@@ -66,6 +66,46 @@ __global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__
   for (int w = 0; w < 4; ++w) X16[4 * i + w] = h[w];
 }
 
+// Prompt activation rows straight to the GEMM's fp16 operand: (bias + GELU table,
+// ggml.c:4113-4152, optional) then quantize_row_q4_0 per 32-block and the dequantized
+// values d*(q-8) as fp16 — what k_q4_quantize + k_act_deq_f16 give, in one pass over the
+// f32 row (which k_gelu would otherwise have read and written once more).  One thread per
+// block.
+__global__ void __launch_bounds__(256) k_act_quant_f16(const float *__restrict__ x, size_t nblk, int nb,
+                                                       const float *__restrict__ bias,
+                                                       const uint16_t *__restrict__ gelu_tab, half8 *__restrict__ X16) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nblk) return;
+  const float4 *src = (const float4 *)(x + i * QK);
+  float v[QK];
+#pragma unroll
+  for (int k = 0; k < QK / 4; ++k) {
+    const float4 t = src[k];
+    v[4 * k] = t.x;
+    v[4 * k + 1] = t.y;
+    v[4 * k + 2] = t.z;
+    v[4 * k + 3] = t.w;
+  }
+  if (gelu_tab) {
+    const int c0 = (int)(i % (size_t)nb) * QK;
+#pragma unroll
+    for (int l = 0; l < QK; ++l) {
+      const float t = bias ? v[l] + bias[c0 + l] : v[l];
+      v[l] = h2f(gelu_tab[f2h(t)]);
+    }
+  }
+  uint32_t w[4];
+  float out[QK];
+  (void)q4_block(v, w, out);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    half8 h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = (_Float16)out[8 * k + e];
+    X16[4 * i + k] = h;
+  }
+}
+
 __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16 *__restrict__ X16, int N,
                                                              const float *__restrict__ bias, float *__restrict__ Y) {
   __shared__ __attribute__((aligned(16))) _Float16 As[GM_BM * GM_LD];
@@ -164,6 +204,35 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16
         }
       }
     }
+}
+
+int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s) {
+  if (K % QK || n <= 0) {
+    set_error("act_quant_f16: K must be a multiple of 32");
+    return VSIM_EINVAL;
+  }
+  const uint16_t *tab = nullptr;
+  if (gelu) {
+    DevTables t;
+    if (int rc = tables_get(&t)) return rc;
+    tab = t.gelu_f16;
+  }
+  const size_t nblk = (size_t)n * (K / QK);
+  hipLaunchKernelGGL(k_act_quant_f16, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, x, nblk, K / QK, bias, tab,
+                     (half8 *)x16);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s) {
+  if (W.k % QK) {
+    set_error("q4 gemm: K must be a multiple of 32");
+    return VSIM_EINVAL;
+  }
+  const dim3 grid((W.rows + GM_BM - 1) / GM_BM, (n + GM_BN - 1) / GM_BN);
+  hipLaunchKernelGGL(k_gemm_q4_f16, grid, dim3(GM_THREADS), 0, s, W, (const _Float16 *)x16, n, bias, y);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
 }
 
 int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s) {

@@ -19,14 +19,16 @@ __host__ __device__ constexpr int xd_slot(int l) { return (l & ~3) | ((l & 1) <<
 // (correctly rounded division), id = 1/d, q = (int8)round(x*id) + 8 with round-half-
 // away-from-zero, nibble pairs (q[2l], q[2l+1]).  Also emits xd = d*(q-8) per element,
 // the activation factor f2/f3 of the reference dot (ggml.c:497-498).
-__device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, float *d_out, float *xd_out) {
+// quantize_row_q4_0 of one 32-block: returns d; w = the 16 packed nibble bytes, out = the
+// dequantized values d*(q-8) (one rounding each, as d*(float)(q-8) in dequantize_row_q4_0).
+__device__ __forceinline__ float q4_block(const float *v, uint32_t w[4], float *out) {
   float amax = 0.0f;
 #pragma unroll
   for (int l = 0; l < QK; ++l) amax = amax > fabsf(v[l]) ? amax : fabsf(v[l]);
   const float d = amax / 7.0f;
   const float id = d != 0.0f ? 1.0f / d : 0.0f;
-  uint32_t w[4] = {0, 0, 0, 0};
-  float out[QK];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = 0;
 #pragma unroll
   for (int l = 0; l < QK; l += 2) {
     const int q0 = x86_round_i8(v[l] * id) + 8;
@@ -35,6 +37,13 @@ __device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, 
     out[l] = d * (float)(q0 - 8);
     out[l + 1] = d * (float)(q1 - 8);
   }
+  return d;
+}
+
+__device__ __forceinline__ void quantize_block(const float *v, uint8_t *qs_out, float *d_out, float *xd_out) {
+  uint32_t w[4];
+  float out[QK];
+  const float d = q4_block(v, w, out);
   *(uint4 *)qs_out = make_uint4(w[0], w[1], w[2], w[3]);
   *d_out = d;
   if (xd_out) {

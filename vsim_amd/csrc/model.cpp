@@ -405,10 +405,11 @@ void bind_pointers(vsim_model *m) {
     if (rc_) return rc_;         \
   } while (0)
 
-// Quantize an activation and run one GEMV in the model's mode.
+// Quantize an activation and run one GEMV in the model's mode.  x16 non-null (fast-mode
+// prompt batches): the activation is already the GEMM's fp16 operand (launch_act_quant_f16).
 int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_t *xq, float *xd, bool quantize,
-       const float *bias, float *y, int &nk) {
-  if (quantize) {
+       const float *bias, float *y, int &nk, const void *x16 = nullptr) {
+  if (quantize && !x16) {
     RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
     ++nk;
   }
@@ -425,7 +426,11 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
     m->prof_used += 2;
     VSIM_HIP(hipEventRecord(ev[0], m->stream));
   }
-  RC(launch_q4_gemv(W, M, K, xq, xd, N, bias, y, m->mode, m->stream));
+  if (x16) {
+    RC(launch_gemm_f16x(w4_view(W, M, K), x16, N, bias, y, m->stream));
+  } else {
+    RC(launch_q4_gemv(W, M, K, xq, xd, N, bias, y, m->mode, m->stream));
+  }
   if (ev) {
     VSIM_HIP(hipEventRecord(ev[1], m->stream));
     m->prof_bytes += (double)M * K / QK * QBYTES;
@@ -467,18 +472,42 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   return VSIM_OK;
 }
 
+// fp16 GEMM operands of a fast-mode prompt layer (stream-ordered, freed on every exit)
+struct PromptX16 {
+  hipStream_t s;
+  void *a = nullptr, *b = nullptr;  // [N][E]: norm outputs; [N][F]: attention / GELU output
+  ~PromptX16() {
+    if (a) (void)hipFreeAsync(a, s);
+    if (b) (void)hipFreeAsync(b, s);
+  }
+};
+
 int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   if (m->arch == VSIM_ARCH_BLOOM) return run_layer_bloom(m, il, n_past, N, nk);
   const LayerW &L = m->layers[il - m->l0];
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E;
   const bool gptj = m->arch == VSIM_ARCH_GPTJ;
   hipStream_t s = m->stream;
+  // fast-mode prompt batch: every activation goes once from f32 to the GEMM's fp16 operand
+  // (quantize_row_q4_0 values, k_act_quant_f16; the GELU folded into fc_out's)
+  PromptX16 X{s};
+  const bool pf = m->mode == VSIM_MODE_FAST && N >= GEMM_MIN_N;
+  if (pf) {
+    VSIM_HIP(hipMallocAsync(&X.a, (size_t)N * E * sizeof(uint16_t), s));
+    VSIM_HIP(hipMallocAsync(&X.b, (size_t)N * F * sizeof(uint16_t), s));
+  }
+  auto act16 = [&](const float *x, int K, void *x16, const float *gbias, bool gelu) -> int {
+    if (!pf) return VSIM_OK;
+    ++nk;
+    return launch_act_quant_f16(x, K, N, gbias, gelu, x16, s);
+  };
   // input LayerNorm + affine (vsim.cpp:526-533)
   RC(launch_norm(m->inpL, m->cur1, E, N, L.ln1_w, L.ln1_b, s)); ++nk;
+  RC(act16(m->cur1, E, X.a, nullptr, false));
   // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
-  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk));
-  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, m->Kb, nk));
-  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, m->Vb, nk));
+  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a));
+  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, m->Kb, nk, X.a));
+  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, m->Vb, nk, X.a));
   // KV write + RoPE (vsim.cpp:553-580)
   const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
   float *kc = m->kcache + loff, *vc = m->vcache + loff;
@@ -499,7 +528,8 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
     RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
     RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
   }
-  RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, gptj ? nullptr : L.bo, m->attn, nk));
+  RC(act16(m->attn_in, E, X.b, nullptr, false));
+  RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, gptj ? nullptr : L.bo, m->attn, nk, X.b));
   // feed-forward input
   const uint8_t *fxq = m->xq1;
   const float *fxd = m->xd1;
@@ -519,9 +549,14 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
     fxd = m->xd2;
     fquant = true;
   }
-  RC(mm(m, L.wfc, F, E, fx, N, (uint8_t *)fxq, (float *)fxd, fquant, nullptr, m->fch, nk));
-  RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
-  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk));
+  if (fquant) RC(act16(fx, E, X.a, nullptr, false));
+  RC(mm(m, L.wfc, F, E, fx, N, (uint8_t *)fxq, (float *)fxd, fquant, nullptr, m->fch, nk, X.a));
+  if (pf) {
+    RC(act16(m->fch, F, X.b, L.bfc, true));  // bias + GELU + quantize, one pass
+  } else {
+    RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
+  }
+  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk, X.b));
   RC(launch_add_residual(m->inpL, m->attn, m->ff, N * E, (!gptj && !m->hp.use_parallel_residual) ? 1 : 0, s)); ++nk;
   return VSIM_OK;
 }

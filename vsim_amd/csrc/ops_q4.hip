@@ -244,7 +244,7 @@ int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s) {
   return VSIM_OK;
 }
 
-constexpr int GEMM_MIN_N = 8;  // fast mode: from this many tokens on, the MFMA GEMM
+// (GEMM_MIN_N, common.hpp: fast mode, from this many tokens on, the MFMA GEMM)
 
 int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias, float *y,
                    int mode, hipStream_t s) {
