@@ -285,3 +285,22 @@ def test_layer_kernel_bit_identical(cfg, tmp_path):
         outs.append(out)
     for other in outs[1:]:
         subprocess.run([sys.executable, tool, "--compare", outs[0], other], check=True, timeout=120)
+
+
+def test_fast_prefill_deterministic_across_processes(tmp_path):
+    """Two fast prompt evals (96 tokens, then 8 on top of the cache) in separate processes give
+    the same logits bits (tools/prefill_ab.py).  In-process repeats reuse every buffer, so
+    they cannot show a dependence on fresh memory; the per-layer stream-ordered operand
+    allocations of an earlier prompt path did show one, in the second eval."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tool = os.path.join(root, "tools", "prefill_ab.py")
+    outs = []
+    for i in range(3):
+        out = str(tmp_path / f"p{i}.npz")
+        subprocess.run([sys.executable, tool, "--file", "--config", "small-gptj", "--n2", "8", "--out", out],
+                       check=True, timeout=300)
+        outs.append(out)
+    for other in outs[1:]:
+        subprocess.run([sys.executable, tool, "--compare", outs[0], other], check=True, timeout=120)

@@ -69,41 +69,23 @@ __global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__
 // Prompt activation rows straight to the GEMM's fp16 operand: (bias + GELU table,
 // ggml.c:4113-4152, optional) then quantize_row_q4_0 per 32-block and the dequantized
 // values d*(q-8) as fp16 — what k_q4_quantize + k_act_deq_f16 give, in one pass over the
-// f32 row (which k_gelu would otherwise have read and written once more).  One thread per
-// block.
+// f32 row (which k_gelu would otherwise have read and written once more).  One value per
+// lane, a half-wave per block (q4_half): coalesced 128-byte reads and 64-byte writes.
 __global__ void __launch_bounds__(256) k_act_quant_f16(const float *__restrict__ x, size_t nblk, int nb,
                                                        const float *__restrict__ bias,
-                                                       const uint16_t *__restrict__ gelu_tab, half8 *__restrict__ X16) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nblk) return;
-  const float4 *src = (const float4 *)(x + i * QK);
-  float v[QK];
-#pragma unroll
-  for (int k = 0; k < QK / 4; ++k) {
-    const float4 t = src[k];
-    v[4 * k] = t.x;
-    v[4 * k + 1] = t.y;
-    v[4 * k + 2] = t.z;
-    v[4 * k + 3] = t.w;
+                                                       const uint16_t *__restrict__ gelu_tab, _Float16 *__restrict__ X16) {
+  const int lane = threadIdx.x & 63;
+  const size_t blk = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool ok = blk < nblk;  // (uniform per half-wave)
+  const size_t e = blk * QK + (lane & 31);
+  float v = ok ? x[e] : 0.0f;
+  if (gelu_tab && ok) {
+    const float t = bias ? v + bias[(int)(blk % (size_t)nb) * QK + (lane & 31)] : v;
+    v = h2f(gelu_tab[f2h(t)]);
   }
-  if (gelu_tab) {
-    const int c0 = (int)(i % (size_t)nb) * QK;
-#pragma unroll
-    for (int l = 0; l < QK; ++l) {
-      const float t = bias ? v[l] + bias[c0 + l] : v[l];
-      v[l] = h2f(gelu_tab[f2h(t)]);
-    }
-  }
-  uint32_t w[4];
-  float out[QK];
-  (void)q4_block(v, w, out);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    half8 h;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = (_Float16)out[8 * k + e];
-    X16[4 * i + k] = h;
-  }
+  float d;
+  const int q = q4_half(v, d);
+  if (ok) X16[e] = (_Float16)(d * (float)(q - 8));
 }
 
 __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16 *__restrict__ X16, int N,
@@ -218,8 +200,8 @@ int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool g
     tab = t.gelu_f16;
   }
   const size_t nblk = (size_t)n * (K / QK);
-  hipLaunchKernelGGL(k_act_quant_f16, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, x, nblk, K / QK, bias, tab,
-                     (half8 *)x16);
+  hipLaunchKernelGGL(k_act_quant_f16, dim3((unsigned)((nblk + 7) / 8)), dim3(256), 0, s, x, nblk, K / QK, bias, tab,
+                     (_Float16 *)x16);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

@@ -342,9 +342,9 @@ __device__ __forceinline__ void st_out(T *p, T v) {
   else *p = v;
 }
 
-template <bool CO = false>
-__device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
-                                              float *xd_out) {
+// quantize_row_q4_0 of one 32-block held one value per lane by a half-wave (lanes 0-31:
+// block A, 32-63: block B): returns the lane's code q (0..15) and the block's scale d.
+__device__ __forceinline__ int q4_half(float v, float &d) {
   // amax over the half-wave: DPP within rows of 16 lanes, then rows 0<->1 and 2<->3 by
   // ds_swizzle (xor 16); no LDS round trips in the dependent chain
   auto mx = [](float a, float b) { return a > b ? a : b; };
@@ -354,9 +354,16 @@ __device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_
   a = mx(a, dpp::mov<dpp::HALF_MIRROR, 0xF>(a, 0.0f));
   a = mx(a, dpp::mov<dpp::MIRROR, 0xF>(a, 0.0f));
   a = mx(a, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(a), 0x401F)));
-  const float d = a / 7.0f;
+  d = a / 7.0f;
   const float id = d != 0.0f ? 1.0f / d : 0.0f;
-  const int q = x86_round_i8(v * id) + 8;
+  return x86_round_i8(v * id) + 8;
+}
+
+template <bool CO = false>
+__device__ __forceinline__ void quantize_half(float v, int lane, bool ok, uint8_t *qs_out, float *d_out,
+                                              float *xd_out) {
+  float d;
+  const int q = q4_half(v, d);
   const int l = lane & 31;
   // byte of pair l/2 (nibbles of lanes 2j, 2j+1), then OR of each 8-lane group's bytes into
   // its word: xor 1, xor 2, and the half-row mirror (lane i <-> 7-i) reach all 8 lanes

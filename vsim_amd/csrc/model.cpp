@@ -100,6 +100,7 @@ struct vsim_model {
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
   float *fast_ffp = nullptr, *fast_part = nullptr;
   void *pf_scratch = nullptr;  // fast prefill: fp16 K / V^T copies (attn_prefill.hip)
+  void *pf_x16 = nullptr;      // fast prefill: fp16 GEMM operands, [n_max][E] then [n_max][4E]
   size_t pf_bytes = 0;
 
   // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
@@ -145,6 +146,8 @@ void free_scratch(vsim_model *m) {
   m->tail_done = nullptr;
   if (m->pf_scratch) (void)hipFree(m->pf_scratch);
   m->pf_scratch = nullptr;
+  if (m->pf_x16) (void)hipFree(m->pf_x16);
+  m->pf_x16 = nullptr;
   m->pf_bytes = 0;
   if (m->fast_ffp) (void)hipFree(m->fast_ffp);
   if (m->fast_part) (void)hipFree(m->fast_part);
@@ -220,6 +223,7 @@ int ensure_scratch(vsim_model *m, int N) {
   {
     const size_t d = E / H, nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
     VSIM_HIP(fa(&m->fast_ffp, 8 * E));
+    if (n >= GEMM_MIN_N) VSIM_HIP(hipMalloc(&m->pf_x16, (size_t)n * (E + F) * sizeof(uint16_t)));
     VSIM_HIP(fa(&m->fast_part, H * nch * (d + 2)));
     VSIM_HIP(hipMemset(m->fast_part, 0, H * nch * (d + 2) * sizeof(float)));  // finite stale values
   }
@@ -472,15 +476,11 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   return VSIM_OK;
 }
 
-// fp16 GEMM operands of a fast-mode prompt layer (stream-ordered, freed on every exit)
-struct PromptX16 {
-  hipStream_t s;
-  void *a = nullptr, *b = nullptr;  // [N][E]: norm outputs; [N][F]: attention / GELU output
-  ~PromptX16() {
-    if (a) (void)hipFreeAsync(a, s);
-    if (b) (void)hipFreeAsync(b, s);
-  }
-};
+static int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e && e[0] ? atoi(e) : dflt;
+}
+
 
 int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   if (m->arch == VSIM_ARCH_BLOOM) return run_layer_bloom(m, il, n_past, N, nk);
@@ -490,12 +490,14 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   hipStream_t s = m->stream;
   // fast-mode prompt batch: every activation goes once from f32 to the GEMM's fp16 operand
   // (quantize_row_q4_0 values, k_act_quant_f16; the GELU folded into fc_out's)
-  PromptX16 X{s};
-  const bool pf = m->mode == VSIM_MODE_FAST && N >= GEMM_MIN_N;
-  if (pf) {
-    VSIM_HIP(hipMallocAsync(&X.a, (size_t)N * E * sizeof(uint16_t), s));
-    VSIM_HIP(hipMallocAsync(&X.b, (size_t)N * F * sizeof(uint16_t), s));
-  }
+  // (operands in the model's scratch, pf_x16: [N][E] norm outputs, then [N][F] attention /
+  // GELU outputs)
+  static const int pf_env = env_int("VSIM_PF_ACT", 1);  // 0: per-GEMM quantize + dequant (A/B)
+  const bool pf = pf_env && m->mode == VSIM_MODE_FAST && N >= GEMM_MIN_N && m->pf_x16;
+  struct {
+    void *a, *b;
+  } X = {m->pf_x16, pf ? (void *)((uint16_t *)m->pf_x16 + (size_t)N * E) : nullptr};
+  if (!pf) X.a = nullptr;
   auto act16 = [&](const float *x, int K, void *x16, const float *gbias, bool gelu) -> int {
     if (!pf) return VSIM_OK;
     ++nk;
@@ -515,7 +517,8 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
-  if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
+  static const int pfa_env = env_int("VSIM_PF_ATT", 1);  // 0: the per-op attention (A/B)
+  if (pfa_env && m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
     // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
     if (!m->pf_scratch) {  // (prompt evals are never graph-captured: allocating here is safe)
       m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
@@ -600,10 +603,6 @@ int fast_sf(const vsim_model *m) {
   return sf;
 }
 
-static int env_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e && e[0] ? atoi(e) : dflt;
-}
 // VSIM_LAYER=1|2 select the one-launch layer kernel (k_layer_exact; 2: fc_in as a launch of
 // its own before it).  Bit-identical to the default three-launch layer, but not faster on
 // GPT-J-6B (489 vs 510 tok/s), so 0 is the default.
