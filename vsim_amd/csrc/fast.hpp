@@ -54,6 +54,8 @@ struct FastGemv {
   // batch is in flight; xq/xd are then unused
   const float *lnx;
   const float *lnw[2], *lnb[2];
+  unsigned *clear;                  // non-null: workgroup 0 zeroes clear[0 .. nclear)
+  int nclear;                       // (the per-head chunk counters of this layer's K2)
 };
 
 struct FastTail {
@@ -69,14 +71,19 @@ struct FastTail {
   const int *npast;
   int d, H, nchunk;
   float scale;
-  float *part;             // [H][nchunk][d + 2]: m, l, o[d] (merged by K3)
+  float *part;             // [H][nchunk][d + 2]: m, l, o[d]
+  // the chunk workgroup of a head that counts last in hcnt[4h] merges the head's chunks
+  // and quantizes the attention output into (oq_qs, oq_d), the out-projection's input
+  unsigned *hcnt;
+  uint8_t *oq_qs;
+  float *oq_d;
 };
 
 struct FastOproj {
   W4 w;                    // out-projection E x E
-  const float *part;       // attention chunk partials (FastTail::part)
-  const int *npast;
-  int d, nchunk;
+  const uint8_t *xq;       // merged attention output, Q4 SoA (FastTail::oq_qs / oq_d)
+  const float *xd;
+  int d;
   const float *bo;         // may be null (GPT-J)
   const float *ffp;        // [sf][E]
   int sf;

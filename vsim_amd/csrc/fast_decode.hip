@@ -348,6 +348,8 @@ __global__ void __launch_bounds__(64 * NW, LNP > 2 ? 5 : 6) k_fast_gemv(FastGemv
   if constexpr (LNP > 0) ln.load(P.lnx, P.lnw[J.act], P.lnb[J.act], nb * QK);
   else st.load(P.xq[J.act], P.xd[J.act], 0, nb);
   const int n_past = J.epi >= FE_ROPE_Q ? *P.npast : 0;
+  if (P.clear && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < P.nclear; i += 64 * NW) P.clear[i] = 0u;
   ts.prefetch();
   if constexpr (LNP > 0) ln.finish(nb * QK, xq, xd, red);
   else st.store(nb, xq, xd);
@@ -407,7 +409,7 @@ constexpr int FT_OCC = 4;
 // row already written by k_fast_gemv's epilogues.  A chunk past n_past writes m = -inf,
 // l = 0, which the merge weighs by zero.
 constexpr int FD_PPW = FD_CHUNK / FD_WAVES;  // positions per wave
-__device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
+__device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {  // (partials stored sc1)
   __shared__ float pr[FD_CHUNK];
   const int d = A.d, E = A.d * A.H, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int e0 = 4 * lane;
@@ -418,8 +420,8 @@ __device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
   float *mine = A.part + ((size_t)h * A.nchunk + c) * (d + 2);
   if (p0 >= nk) {
     if (tid == 0) {
-      mine[0] = -INFINITY;
-      mine[1] = 0.0f;
+      st_out<true>(mine, -INFINITY);
+      st_out<true>(mine + 1, 0.0f);
     }
     return;
   }
@@ -459,8 +461,8 @@ __device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
     const float l = wave_sum_f(e);
     pr[lane] = e;
     if (lane == 0) {
-      mine[0] = m;
-      mine[1] = l;
+      st_out<true>(mine, m);
+      st_out<true>(mine + 1, l);
     }
   }
   __syncthreads();
@@ -479,21 +481,36 @@ __device__ void fast_attn_chunk(const FastTail &A, int h, int c, float *ored) {
     float v = 0.0f;
 #pragma unroll
     for (int w = 0; w < FD_WAVES; ++w) v += ored[w * 256 + i];
-    mine[2 + i] = v;
+    st_out<true>(mine + 2 + i, v);
   }
 }
 
 __device__ __forceinline__ void fast_fcout_part(const FastTail &A, int idx, uint4 *xq, float *xd,
                                                 float (*part)[T32]);
+__device__ void fast_merge_head(const FastTail &A, int h, int lane);
 
 __global__ void __launch_bounds__(FT_NT, FT_OCC) k_fast_tail(FastTail A) {
   __shared__ uint4 xq[FD_MAXE / QK];
   __shared__ float xd[FD_MAXE / QK];
   __shared__ float part[2 * FD_WAVES][T32];
   __shared__ float ored[FD_WAVES * 256];
+  __shared__ int last;
   const int na = A.H * A.nchunk;
   if ((int)blockIdx.x < na) {
-    fast_attn_chunk(A, blockIdx.x / A.nchunk, blockIdx.x % A.nchunk, ored);
+    const int h = blockIdx.x / A.nchunk;
+    fast_attn_chunk(A, h, blockIdx.x % A.nchunk, ored);
+    // counter hand-off (cdna_hip_programming.md §6 Guideline 16): every wave drains its sc1
+    // partial stores, one lane counts; the head's last chunk workgroup acquires and merges
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(A.hcnt + 4 * h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned)A.nchunk - 1;
+    __syncthreads();
+    if (last && threadIdx.x < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      fast_merge_head(A, h, threadIdx.x);
+    }
     return;
   }
   fast_fcout_part(A, blockIdx.x - na, xq, xd, part);
@@ -523,67 +540,43 @@ __device__ __forceinline__ void fast_fcout_part(const FastTail &A, int idx, uint
   if (wave == 0 && lane < T32) A.ffp[(size_t)sp * A.wf.rows + t * T32 + lane] = s;
 }
 
-// ------------------------------------------------------------------ K3: out-proj + join
-// Every workgroup first merges the attention chunks of all heads (chunk c of head h:
-// m = max score, l = sum e^(s - m), o = sum e^(s - m) v) into the attention output
-// sum_c o_c e^(m_c - M) / sum_c l_c e^(m_c - M) and quantizes it into LDS.
-// Merge over all nchunk chunks, FD_MG at a time, with every load of a group (the chunks'
-// m, l and this thread's o values) issued together; chunks past n_past weigh zero.
-constexpr int FD_MAXW = 4096;  // merge weights in LDS: heads x chunks
-constexpr int FD_MG = 8;       // chunks per load group
-template <int NT>
-__device__ __forceinline__ void attn_merge_lds(const FastOproj &P, int E, uint4 *xq, float *xd, float *wgt) {
-  const int tid = threadIdx.x, d = P.d, H = E / d, nch = P.nchunk;
-  const int nv = min(*P.npast / FD_CHUNK + 1, nch);  // chunks holding positions 0 .. n_past
-  // (m, l) of every (head, chunk) into LDS: wgt[h*nch + c] = m, wgt[H*nch + h*nch + c] = l
-  for (int x = tid; x < H * nch; x += NT) {
-    const float *pc = P.part + (size_t)x * (d + 2);
-    wgt[x] = pc[0];
-    wgt[H * nch + x] = pc[1];
+// ------------------------------------------------------------------ attention merge
+// Head h's chunks (chunk c: m = max score, l = sum e^(s - m), o = sum e^(s - m) v) into the
+// attention output sum_c o_c e^(m_c - M) / sum_c l_c e^(m_c - M), quantized into the
+// out-projection's Q4 input.  Run by wave 0 of the chunk workgroup that counts last for the
+// head, behind one agent acquire (the partials were stored sc1).  Four consecutive outputs
+// per lane, a 32-block = 8 lanes; chunks past n_past weigh zero.
+constexpr int FD_MAXCH = 64;  // chunks per head (n_ctx <= 4096)
+__device__ void fast_merge_head(const FastTail &A, int h, int lane) {
+  const int d = A.d, nch = A.nchunk;
+  const int nv = min(*A.npast / FD_CHUNK + 1, nch);  // chunks holding positions 0 .. n_past
+  const float *ph = A.part + (size_t)h * nch * (d + 2);
+  float M = -INFINITY;
+  for (int c = 0; c < nch; ++c) M = fmaxf(M, ph[(size_t)c * (d + 2)]);
+  float L = 0.0f;
+  for (int c = 0; c < nch; ++c) {
+    const float e = __expf(ph[(size_t)c * (d + 2)] - M);
+    L = __builtin_fmaf(ph[(size_t)c * (d + 2) + 1], e, L);
   }
-  __syncthreads();
-  for (int h = tid; h < H; h += NT) {  // weights e^(m_c - M) / sum_c l_c e^(m_c - M)
-    float M = -INFINITY;
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, wgt[h * nch + c]);
-    float L = 0.0f;
-    for (int c = 0; c < nch; ++c) {
-      const float e = __expf(wgt[h * nch + c] - M);
-      wgt[h * nch + c] = e;
-      L = __builtin_fmaf(wgt[H * nch + h * nch + c], e, L);
-    }
-    const float inv = 1.0f / L;
-    for (int c = 0; c < nch; ++c) wgt[h * nch + c] *= inv;
+  const float inv = 1.0f / L;
+  const int i = 4 * lane;
+  const bool ok = i < d;  // 8-lane uniform (d % 32 == 0)
+  float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c = 0; c < nv; ++c) {
+    const float w = __expf(ph[(size_t)c * (d + 2)] - M) * inv;
+    const float4 o = ok ? *(const float4 *)(ph + (size_t)c * (d + 2) + 2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    y.x = __builtin_fmaf(o.x, w, y.x);
+    y.y = __builtin_fmaf(o.y, w, y.y);
+    y.z = __builtin_fmaf(o.z, w, y.z);
+    y.w = __builtin_fmaf(o.w, w, y.w);
   }
-  __syncthreads();
-  // four consecutive outputs per thread (one head), a 32-block = 8 lanes
-  for (int base = 0; base < E; base += 4 * NT) {
-    const int i = base + 4 * tid;
-    const bool ok = i < E;  // 8-lane uniform (E % 32 == 0)
-    const int ic = ok ? i : 0, h = ic / d;
-    const float *src = P.part + (size_t)h * nch * (d + 2) + 2 + (ic - h * d);
-    float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c0 = 0; c0 < nv; c0 += FD_MG) {  // chunks past n_past weigh zero: skipped
-      float4 o[FD_MG];
-#pragma unroll
-      for (int u = 0; u < FD_MG; ++u)
-        o[u] = c0 + u < nv ? *(const float4 *)(src + (size_t)(c0 + u) * (d + 2)) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int u = 0; u < FD_MG; ++u) {
-        const float w = c0 + u < nv ? wgt[h * nch + c0 + u] : 0.0f;
-        y.x = __builtin_fmaf(o[u].x, w, y.x);
-        y.y = __builtin_fmaf(o[u].y, w, y.y);
-        y.z = __builtin_fmaf(o[u].z, w, y.z);
-        y.w = __builtin_fmaf(o[u].w, w, y.w);
-      }
-    }
-    fq_oct(y, tid & 63, ok, (uint8_t *)&xq[ic / QK], &xd[ic / QK], 0x8888u);
-  }
+  const int blk = (h * d + (ok ? i : 0)) / QK;
+  fq_oct(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk);
 }
 
 // Out-projection tile t and the residual join (K3).
 template <int NW>
-__device__ __forceinline__ void fast_oproj_tile(const FastOproj &P, int t, uint4 *xq, float *xd, float (*part)[T32],
-                                                float *wgt) {
+__device__ __forceinline__ void fast_oproj_tile(const FastOproj &P, int t, uint4 *xq, float *xd, float (*part)[T32]) {
   const int nb = P.w.nb(), E = P.w.rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   TileStream<> ts;
@@ -592,8 +585,10 @@ __device__ __forceinline__ void fast_oproj_tile(const FastOproj &P, int t, uint4
   ts.b0 = wave * nb / NW;
   ts.b1 = (wave + 1) * nb / NW;
   ts.lane = lane;
+  ActStage st;
+  st.load(P.xq, P.xd, 0, nb);
   ts.prefetch();
-  attn_merge_lds<64 * NW>(P, E, xq, xd, wgt);
+  st.store(nb, xq, xd);
   __syncthreads();
   const float acc = ts.run(xq, xd);
   const float s = tile_reduce<NW>(acc, part);
@@ -610,8 +605,7 @@ __global__ void __launch_bounds__(64 * FD_OWAVES) k_fast_oproj_join(FastOproj P)
   __shared__ uint4 xq[FD_MAXE / QK];
   __shared__ float xd[FD_MAXE / QK];
   __shared__ float part[2 * FD_OWAVES][T32];
-  __shared__ float wgt[FD_MAXW];
-  fast_oproj_tile<FD_OWAVES>(P, blockIdx.x, xq, xd, part, wgt);
+  fast_oproj_tile<FD_OWAVES>(P, blockIdx.x, xq, xd, part);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -651,8 +645,8 @@ int launch_fast_gemv(const FastGemv &P, int E, hipStream_t s) {
 
 int launch_fast_tail(const FastTail &A, hipStream_t s) {
   if (A.d > 256 || A.d % QK != 0 || A.wf.k / A.sf > FD_MAXE || A.wf.nb() % A.sf != 0 ||
-      A.wf.nb() / A.sf > FT_NT) {
-    set_error("fast decode: unsupported head dim or fc_out split");
+      A.wf.nb() / A.sf > FT_NT || A.nchunk > FD_MAXCH || !A.hcnt) {
+    set_error("fast decode: unsupported head dim, fc_out split or context length");
     return VSIM_EINVAL;
   }
   const int grid = A.H * A.nchunk + A.wf.tiles * A.sf;
@@ -662,7 +656,7 @@ int launch_fast_tail(const FastTail &A, hipStream_t s) {
 }
 
 int launch_fast_oproj_join(const FastOproj &P, hipStream_t s) {
-  if (P.w.k > FD_MAXE || P.w.nb() > 64 * FD_OWAVES || P.w.rows != P.w.k || 2 * (P.w.k / P.d) * P.nchunk > FD_MAXW) {
+  if (P.w.k > FD_MAXE || P.w.nb() > 64 * FD_OWAVES || P.w.rows != P.w.k) {
     set_error("fast decode: out-projection K too large");
     return VSIM_EINVAL;
   }

@@ -691,6 +691,8 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     P.j[2] = FastJob{w4_view(L.wk, E, E), gptj ? nullptr : L.bk, m->kcache + loff, FE_ROPE_K, 0};
     P.j[3] = FastJob{w4_view(L.wv, E, E), gptj ? nullptr : L.bv, m->vcache + loff, FE_V, 0};
     P.gelu_tab = tab.gelu_f16;
+    P.clear = m->tail_done;  // K2's per-head counters (tail_done[4h])
+    P.nclear = 4 * H;
     P.oq_qs = q3;
     P.oq_d = d3;
     P.npast = m->npast_dev;
@@ -718,13 +720,15 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     T.nchunk = nchunk;
     T.scale = scale;
     T.part = m->fast_part;
+    T.hcnt = m->tail_done;
+    T.oq_qs = m->xqa;
+    T.oq_d = (float *)(m->xqa + (size_t)(E / QK) * 16);
     // attention merge + out-projection + residual join into the other buffer
     FastOproj O{};
     O.w = w4_view(L.wo, E, E);
-    O.part = m->fast_part;
-    O.npast = m->npast_dev;
+    O.xq = T.oq_qs;
+    O.xd = T.oq_d;
     O.d = d;
-    O.nchunk = nchunk;
     O.bo = gptj ? nullptr : L.bo;
     O.ffp = m->fast_ffp;
     O.sf = fast_sf(m);
