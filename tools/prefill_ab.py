@@ -31,7 +31,7 @@ def main():
     from vsim_amd import hip
     from vsim_amd import modelgen as mg
     arch_s, hp = mg.CONFIGS[args.config]
-    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    arch = {"gptj": hip.ARCH_GPTJ, "gptneox": hip.ARCH_GPTNEOX, "bloom": hip.ARCH_BLOOM}[arch_s]
     if args.file:
         import tempfile
         path = os.path.join(tempfile.mkdtemp(), "pf.bin")

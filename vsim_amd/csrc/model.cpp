@@ -450,10 +450,20 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   const LayerW &L = m->layers[il - m->l0];
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E;
   hipStream_t s = m->stream;
+  // fast-mode prompt batch: GEMM operands straight to fp16 in the model's scratch (as run_layer)
+  const bool pf = m->mode == VSIM_MODE_FAST && N >= GEMM_MIN_N && m->pf_x16;
+  void *xa = pf ? m->pf_x16 : nullptr;
+  void *xb = pf ? (void *)((uint16_t *)m->pf_x16 + (size_t)N * E) : nullptr;
+  auto act16 = [&](const float *x, int K, void *x16, const float *gbias, bool gelu) -> int {
+    if (!pf) return VSIM_OK;
+    ++nk;
+    return launch_act_quant_f16(x, K, N, gbias, gelu, x16, s);
+  };
   RC(launch_norm(m->inpL, m->cur1, E, N, L.ln1_w, L.ln1_b, s)); ++nk;
-  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, L.bq, m->Qb, nk));
-  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bk, m->Kb, nk));
-  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bv, m->Vb, nk));
+  RC(act16(m->cur1, E, xa, nullptr, false));
+  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, L.bq, m->Qb, nk, xa));
+  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bk, m->Kb, nk, xa));
+  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bv, m->Vb, nk, xa));
   const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
   float *kc = m->kcache + loff, *vc = m->vcache + loff;
   RC(launch_rope_kv_write(0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, 0, m->rope_cs, s)); ++nk;  // no rotary
@@ -462,14 +472,20 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
   RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s, m->alibi)); ++nk;
   RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
-  RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, L.bo, m->attn, nk));
+  RC(act16(m->attn_in, E, xb, nullptr, false));
+  RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, L.bo, m->attn, nk, xb));
   // inpFF = attn + inpL (kept in cur2), its LayerNorm into cur1
   VSIM_HIP(hipMemcpyAsync(m->cur2, m->attn, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
   RC(launch_add_bias(m->cur2, m->inpL, N * E, 1, s)); ++nk;
   RC(launch_norm(m->cur2, m->cur1, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
-  RC(mm(m, L.wfc, F, E, m->cur1, N, m->xq2, m->xd2, true, nullptr, m->fch, nk));
-  RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
-  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk));
+  RC(act16(m->cur1, E, xa, nullptr, false));
+  RC(mm(m, L.wfc, F, E, m->cur1, N, m->xq2, m->xd2, true, nullptr, m->fch, nk, xa));
+  if (pf) {
+    RC(act16(m->fch, F, xb, L.bfc, true));  // bias + GELU + quantize, one pass
+  } else {
+    RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
+  }
+  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk, xb));
   // inpL = ff + inpFF
   VSIM_HIP(hipMemcpyAsync(m->inpL, m->cur2, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
   RC(launch_add_bias(m->inpL, m->ff, N * E, 1, s)); ++nk;
