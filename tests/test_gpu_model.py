@@ -112,6 +112,23 @@ def test_fast_mode_tracks_exact(tmp_path):
     assert cos > 0.95, cos
 
 
+def test_bloom_fast_prefill_tracks_exact(tmp_path):
+    """BLOOM's prompt layer in fast mode (fp16 MFMA GEMMs on the activation operands of
+    k_act_quant_f16, GELU folded into fc_out's) stays close to exact mode (cos > 0.95)."""
+    arch_s, hp = mg.CONFIGS["small-bloom"]
+    path = str(tmp_path / "bpf.bin")
+    mg.write_model(path, arch_s, hp, seed=6, std=0.05)
+    ids = [(29 * i + 3) % hp.n_vocab for i in range(40)]
+    me = hip.Model.load(path, hip.ARCH_BLOOM)
+    me.set_mode(hip.MODE_EXACT)
+    le = me.eval(0, ids)
+    mf = hip.Model.load(path, hip.ARCH_BLOOM)
+    mf.set_mode(hip.MODE_FAST)
+    lf = mf.eval(0, ids)
+    cos = float(np.dot(le, lf) / (np.linalg.norm(le) * np.linalg.norm(lf)))
+    assert cos > 0.95, cos
+
+
 @pytest.mark.parametrize("arch_name", ["small-gptj", "small-neox"])
 def test_fast_prefill_deterministic(arch_name, tmp_path):
     """The fast prompt path (activations quantized straight to fp16, MFMA GEMM, MFMA
