@@ -1,4 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread -k "bloom_fast" > gpurun_out/bt.log 2>&1 || { tail -20 gpurun_out/bt.log; exit 1; }
-tail -1 gpurun_out/bt.log
+o=gpurun_out
+: > $o/other.jsonl
+for c in pythia-12b gpt-neoxt-20b bloom-560m; do for md in exact fast; do
+timeout -k 10 400 python3 bench.py --config $c --mode $md --no-cpu-baseline --no-fast --steps 128 > $o/oc.log 2>&1 || { tail -5 $o/oc.log; exit 1; }
+tail -1 $o/oc.log >> $o/other.jsonl; tail -1 $o/oc.log | cut -c1-140
+done; done
