@@ -1,8 +1,3 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-o=gpurun_out
-: > $o/other.jsonl
-for c in pythia-12b gpt-neoxt-20b bloom-560m; do for md in exact fast; do
-timeout -k 10 400 python3 bench.py --config $c --mode $md --no-cpu-baseline --no-fast --steps 128 > $o/oc.log 2>&1 || { tail -5 $o/oc.log; exit 1; }
-tail -1 $o/oc.log >> $o/other.jsonl; tail -1 $o/oc.log | cut -c1-140
-done; done
+for lib in vsim_amd/_build/libvsim_hip.so vsim_amd/_build/var/u8o2.so vsim_amd/_build/var/u4o3.so vsim_amd/_build/var/u8o3.so vsim_amd/_build/libvsim_hip.so; do echo "== $lib"; VSIM_LIB=$lib timeout -k 10 300 python3 bench.py --mode fast --no-cpu-baseline --no-profile 2>&1 | tail -1 | cut -c90-150 || exit 1; done
