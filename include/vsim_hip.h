@@ -135,6 +135,8 @@ int vsim_model_load_file(const char *path, int arch, int n_ctx, int device, int 
                          vsim_model **out);
 /* Upload one tensor by its ggml-file name (Q4_0 tensors in the on-disk AoS format). */
 int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes);
+/* Read one tensor back in the same file format (Q4_0 as AoS blocks, F32 as floats). */
+int vsim_model_get_tensor(vsim_model *m, const char *name, void *host, size_t nbytes);
 /* Synthetic weights drawn on the device (N(0,std), LN gains 1+N(0,std)), quantized with
  * quantize_row_q4_0 semantics; for throughput runs of full-size configs. */
 int vsim_model_randomize(vsim_model *m, uint64_t seed, float std);
@@ -163,10 +165,15 @@ const float *vsim_model_logits_dev(vsim_model *m);
 /* Number of kernels one eval launches; whether the decode step replays a hipGraph. */
 int vsim_model_info(vsim_model *m, int *kernels_per_eval, int *graph_enabled, size_t *weight_bytes);
 int vsim_model_set_graph(vsim_model *m, int enable);
-/* GEMV profiling for the live roofline: when enabled, an event pair brackets every Q4_0
- * GEMV launch on the model's stream; stats accumulate the summed GEMV device time, the
- * launch count and the algorithmic weight bytes those launches read. */
+/* Per-kernel profiling for the live roofline: when enabled (this resets the totals), the
+ * decode step runs without its hipGraph and an event pair on the model's stream brackets
+ * every launch, tagged with the kernel's name and the algorithmic bytes it moves (Q4_0
+ * weights at 0.625 B/weight, KV rows read and written, LayerNorm rows).
+ * profile_kernel(i): totals of the i-th kernel name seen (VSIM_EINVAL past the last);
+ * profile_stats: the sums over all of them. */
 int vsim_model_set_profile(vsim_model *m, int enable);
+int vsim_model_profile_kernel(vsim_model *m, int i, char *name, int name_cap, double *ms, long *launches,
+                              double *bytes);
 int vsim_model_profile_stats(vsim_model *m, double *gemv_ms, long *gemv_launches, double *gemv_bytes);
 void vsim_model_free(vsim_model *m);
 

@@ -320,6 +320,10 @@ bool read_all(std::ifstream &f, void *p, size_t n) {
   return (size_t)f.gcount() == n;
 }
 
+using SlotMap = std::map<std::string, std::pair<void *, size_t>>;
+void build_slots(Model *m, SlotMap &slots);
+bool read_tensors(std::ifstream &f, SlotMap &slots);
+
 // vsim.cpp:108-458 (GPT-NeoX) and convert_gptj_to_ggml.py:106-126 (GPT-J) formats.
 Model *load_model(const char *path, int arch, int n_ctx) {
   std::ifstream f(path, std::ios::binary);
@@ -351,9 +355,24 @@ Model *load_model(const char *path, int arch, int n_ctx) {
     std::string w(len, 0);
     read_all(f, &w[0], len);
   }
+  SlotMap slots;
+  build_slots(m, slots);
+  if (!read_tensors(f, slots)) {
+    delete m;
+    return nullptr;
+  }
+  m->mem_k.assign((size_t)m->n_layer * n_ctx * m->n_embd, 0.0f);
+  m->mem_v.assign((size_t)m->n_layer * n_ctx * m->n_embd, 0.0f);
+  return m;
+}
+
+// name -> (vector, kind 0 = F32 / 1 = Q4_0), each vector sized to its tensor.  Names of
+// vsim.cpp:287-346 (GPT-NeoX), HF GPTJForCausalLM via convert_gptj_to_ggml.py, and
+// convert_bloom_to_ggml.py:22-34 (BLOOM).
+void build_slots(Model *m, SlotMap &slots) {
   const int E = m->n_embd, L = m->n_layer, V = m->n_vocab;
+  const int arch = m->arch;
   m->layers.resize(L);
-  std::map<std::string, std::pair<void *, size_t>> slots;  // name -> (vector ptr, elem bytes kind)
   auto f32slot = [&](const std::string &n, std::vector<float> &v, size_t ne) { v.resize(ne); slots[n] = {&v, 0}; };
   auto q4slot = [&](const std::string &n, std::vector<uint8_t> &v, size_t ne) { v.resize(ne / QK * QBYTES); slots[n] = {&v, 1}; };
   if (arch == VO_ARCH_GPTNEOX) {
@@ -425,11 +444,18 @@ Model *load_model(const char *path, int arch, int n_ctx) {
       f32slot(p + "mlp.fc_out.bias", l.bproj, E);
     }
   }
+}
+
+// Tensor records until EOF (vsim.cpp:375-448): every one must name a slot of the right type
+// and size.
+bool read_tensors(std::ifstream &f, SlotMap &slots) {
   while (true) {
     int32_t n_dims, length, ftype;
     if (!read_all(f, &n_dims, 4)) break;
+    if (n_dims < 1 || n_dims > 4) return false;
     read_all(f, &length, 4);
     read_all(f, &ftype, 4);
+    if (length <= 0 || length > 1024) return false;
     size_t ne = 1;
     for (int i = 0; i < n_dims; ++i) {
       int32_t d;
@@ -441,22 +467,17 @@ Model *load_model(const char *path, int arch, int n_ctx) {
     auto it = slots.find(name);
     if (it == slots.end()) {
       fprintf(stderr, "oracle: unknown tensor '%s'\n", name.c_str());
-      delete m;
-      return nullptr;
+      return false;
     }
     if (it->second.second == 0) {
       auto *v = (std::vector<float> *)it->second.first;
-      if (ftype != 0 || v->size() != ne) { delete m; return nullptr; }
-      read_all(f, v->data(), ne * 4);
+      if (ftype != 0 || v->size() != ne || !read_all(f, v->data(), ne * 4)) return false;
     } else {
       auto *v = (std::vector<uint8_t> *)it->second.first;
-      if (ftype != 2 || v->size() != ne / QK * QBYTES) { delete m; return nullptr; }
-      read_all(f, v->data(), v->size());
+      if (ftype != 2 || v->size() != ne / QK * QBYTES || !read_all(f, v->data(), v->size())) return false;
     }
   }
-  m->mem_k.assign((size_t)L * n_ctx * E, 0.0f);
-  m->mem_v.assign((size_t)L * n_ctx * E, 0.0f);
-  return m;
+  return true;
 }
 
 void affine(std::vector<float> &x, const std::vector<float> &w, const std::vector<float> &b, int E, int N) {
@@ -791,6 +812,41 @@ void *vo_model_synthetic(int arch, int n_vocab, int n_embd, int n_head, int n_la
   m->mem_k.assign((size_t)n_layer * n_ctx * E, 0.0f);
   m->mem_v.assign((size_t)n_layer * n_ctx * E, 0.0f);
   return m;
+}
+
+// An empty model of the given shape whose tensors are then set one by one by name
+// (vo_model_set_tensor): the parity tests copy a device model's weights in.
+void *vo_model_create(int arch, int n_vocab, int n_embd, int n_head, int n_layer, int n_rot, int par_res, int n_ctx) {
+  init_tables_once();
+  auto *m = new Model();
+  m->arch = arch;
+  m->n_vocab = n_vocab; m->n_embd = n_embd; m->n_head = n_head; m->n_layer = n_layer;
+  m->n_rot = arch == VO_ARCH_BLOOM ? 0 : n_rot;
+  m->par_res = arch == VO_ARCH_BLOOM ? 0 : arch == VO_ARCH_GPTJ ? 1 : par_res;
+  m->ftype = 2; m->n_ctx = n_ctx;
+  SlotMap slots;
+  build_slots(m, slots);
+  m->mem_k.assign((size_t)n_layer * n_ctx * n_embd, 0.0f);
+  m->mem_v.assign((size_t)n_layer * n_ctx * n_embd, 0.0f);
+  return m;
+}
+/* Q4_0 tensors in the file's AoS blocks, F32 as floats; -1: unknown name or wrong size */
+int vo_model_set_tensor(void *mp, const char *name, const void *data, size_t nbytes) {
+  auto *m = (Model *)mp;
+  SlotMap slots;
+  build_slots(m, slots);  // (same sizes again: the vectors keep what is already set)
+  auto it = slots.find(name);
+  if (it == slots.end()) return -1;
+  if (it->second.second == 0) {
+    auto *v = (std::vector<float> *)it->second.first;
+    if (v->size() * 4 != nbytes) return -1;
+    std::memcpy(v->data(), data, nbytes);
+  } else {
+    auto *v = (std::vector<uint8_t> *)it->second.first;
+    if (v->size() != nbytes) return -1;
+    std::memcpy(v->data(), data, nbytes);
+  }
+  return 0;
 }
 
 void vo_model_hparams(void *mp, int32_t *o) {

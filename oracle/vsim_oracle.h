@@ -56,6 +56,10 @@ void vo_get_rows_q4_0(const void *W, int K, const int32_t *rows, int n, float *y
 void *vo_model_load(const char *path, int arch, int n_ctx);
 void *vo_model_synthetic(int arch, int n_vocab, int n_embd, int n_head, int n_layer, int n_rot, int n_ctx,
                          uint64_t seed, float stddev);
+/* an empty model of this shape; tensors then set by their ggml-file names (Q4_0 as AoS
+ * blocks, F32 as floats); set_tensor returns -1 for an unknown name or a wrong size */
+void *vo_model_create(int arch, int n_vocab, int n_embd, int n_head, int n_layer, int n_rot, int par_res, int n_ctx);
+int   vo_model_set_tensor(void *m, const char *name, const void *data, size_t nbytes);
 void  vo_model_hparams(void *m, int32_t *out8); /* n_vocab n_embd n_head n_layer n_rot par_res ftype n_ctx */
 int   vo_model_eval(void *m, int n_past, const int32_t *tokens, int N, float *logits, int nthreads);
 /* run only layers [l0,l1) + optional head on a prepared residual (cpu_baseline sampling) */

@@ -28,6 +28,9 @@ def lib():
         L.vo_model_eval.argtypes = [vp, ci, vp, ci, vp, ci]
         L.vo_model_synthetic.restype = vp
         L.vo_model_synthetic.argtypes = [ci, ci, ci, ci, ci, ci, ci, ctypes.c_uint64, cf]
+        L.vo_model_create.restype = vp
+        L.vo_model_create.argtypes = [ci, ci, ci, ci, ci, ci, ci, ci]
+        L.vo_model_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_size_t]
         L.vo_model_hparams.argtypes = [vp, vp]
         L.vo_model_free.argtypes = [vp]
         L.vo_generate.argtypes = [vp, vp, ci, ci, ci, ci, cf, cf, ci, cf, ci, vp, ci, ci]
@@ -155,6 +158,29 @@ class Model:
         hp = np.zeros(8, np.int32)
         lib().vo_model_hparams(self.h, p(hp))
         self.n_vocab, self.n_embd, self.n_head, self.n_layer, self.n_rot = (int(v) for v in hp[:5])
+
+    @classmethod
+    def from_device(cls, dm, arch_s: str, n_ctx: int = 512):
+        """An oracle model holding exactly the weights of the device model `dm` (read back
+        through vsim_model_get_tensor, i.e. unpacked from the device layout)."""
+        import sys
+        sys.path.insert(0, ROOT)
+        from vsim_amd import modelgen as mg
+        hp = dm.hp
+        self = cls.__new__(cls)
+        arch = {"gptneox": 0, "gptj": 1, "bloom": 2}[arch_s]
+        self.h = lib().vo_model_create(arch, hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot,
+                                       hp.use_parallel_residual, n_ctx)
+        mhp = mg.HParams(hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot, hp.use_parallel_residual)
+        for name, ne, kind in mg.tensor_specs(arch_s, mhp):
+            n = int(np.prod(ne))
+            nbytes = n // 32 * 20 if kind == "q" else 4 * n
+            buf = dm.get_tensor(name, nbytes)
+            if lib().vo_model_set_tensor(self.h, name.encode(), p(buf), nbytes) != 0:
+                raise RuntimeError(f"oracle set_tensor {name}")
+        self.n_vocab, self.n_embd, self.n_head, self.n_layer, self.n_rot = (
+            hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot)
+        return self
 
     def eval(self, n_past, tokens, nthreads=1):
         t = np.ascontiguousarray(tokens, np.int32)

@@ -202,14 +202,28 @@ def test_get_rows_bit_exact():
     assert np.array_equal(bits(host(y)), bits(z["y"]))
 
 
-@pytest.mark.parametrize("M,K", [(4096, 4096), (1024, 16384), (50400, 256)])
+def rand_q4_aos(rng, M, K, std=0.02):
+    """Random Q4_0 rows straight as AoS blocks (uniform nibbles, scales |N(0, 1)| * std / 3):
+    the shape of a quantized weight without quantizing hundreds of millions of floats."""
+    nblk = M * K // 32
+    out = np.empty((nblk, 20), np.uint8)
+    out[:, :4] = (np.abs(rng.standard_normal(nblk, dtype=np.float32)) * np.float32(std / 3)).view(np.uint8).reshape(-1, 4)
+    out[:, 4:] = rng.integers(0, 256, (nblk, 16), dtype=np.uint8)
+    return out.reshape(-1)
+
+
+# Shapes and the kernel launch_gemv_chain_batch picks for them (gemv_chain.hip): >= 192
+# 64-row groups -> k_gemv_solo (the bench's Q/K/V + fc_in batch, 28672 x 4096, and the heads),
+# fewer -> k_gemv_chain32 (fc_out, out-projection).
+@pytest.mark.parametrize("M,K", [(4096, 4096), (1024, 16384), (50400, 256), (16384, 4096), (28672, 4096),
+                                 (50400, 4096), (50432, 6144), (250880, 1024), (6144, 24576), (4064, 4096)])
 def test_gemv_exact_full_width_vs_oracle(M, K):
-    """GPT-J widths (K = n_embd and 4*n_embd, V rows) against the CPU restatement."""
+    """GPT-J / 20B / BLOOM widths (K = n_embd and 4*n_embd, V rows) against the CPU restatement."""
     import oracle_py as O
     rng = np.random.default_rng(M + K)
-    aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))
+    aos = rand_q4_aos(rng, M, K)
     x = rng.standard_normal(K).astype(np.float32)
-    ref = O.mul_mat(aos, M, K, x, 1, nthreads=8)
+    ref = O.mul_mat(aos, M, K, x, 1, nthreads=16)
     w = repack(aos, M, K)
     xq, xd = quantize(x, K, 1)
     assert np.array_equal(bits(gemv(w, M, K, xq, xd, 1, hip.MODE_EXACT)), bits(ref))

@@ -21,13 +21,12 @@ constexpr int ATT_KB = 4;       // KQ: four-key steps per wave per load batch
 constexpr int ATT_DPL = 4;      // max float4 of the head dimension per lane in KQ (d <= 256)
 
 // One head (h) per workgroup of NT >= d threads; sm: attn_lds_floats(d, n_ctx) floats of LDS.
-// prof (timing experiments only): s_memtime stamps of head 0's phases, thread 0
 // Work item hs = head * S + part, S = A.nsplit (>= 1): every part computes the head's scores
 // and softmax (identical in each), then the KQV chains and quantization of output columns
 // [part*c, part*c + c), c = d / S, so a head's V rows spread over S CUs.  Every part writes
 // the same new K/V cache row (identical bytes) before reading it back.
 template <int NT, bool CO = false>
-__device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, unsigned long long *prof = nullptr) {
+__device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   constexpr int ATT_THREADS = NT, ATT_WAVES = NT / 64;
   const int S = A.nsplit > 1 ? A.nsplit : 1, h = hs / S, part = hs % S;
   const int d = A.d, E = A.d * A.H, c = d / S, c0 = part * c;
@@ -39,8 +38,6 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, u
   __shared__ float shf[ATT_WAVES];
   __shared__ double shd[ATT_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  prof = part == 0 ? prof : nullptr;
-  if (prof && h == 0 && tid == 0) prof[0] = __builtin_amdgcn_s_memtime();
   for (int i = tid; i < d; i += ATT_THREADS) {
     qh[i] = A.q[h * d + i];
     kh[i] = A.k[h * d + i];
@@ -67,7 +64,6 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, u
   }
   __syncthreads();
   for (int i = tid; i < d; i += ATT_THREADS) A.kc[(size_t)n_past * E + h * d + i] = kh[i];
-  if (prof && h == 0 && tid == 0) prof[1] = __builtin_amdgcn_s_memtime();
   // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale.
   // Row r (lanes 16r..16r+15) of a wave takes one key per step; lane l16 covers the float4s
   // at 4*l16 + 64*e of the head dimension.  A wave loads ATT_KB steps (4*ATT_KB keys) at once.
@@ -132,7 +128,6 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, u
     }
   }
   // max, exp via table, exact double sum (fp16 values: any order), 1/sum
-  if (prof && h == 0 && tid == 0) prof[2] = __builtin_amdgcn_s_memtime();
   mx = wave_max_f(mx);
   if (lane == 0) shf[wid] = mx;
   __syncthreads();
@@ -152,7 +147,6 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, u
   const float inv = (float)(1.0 / sum);
   for (int k = tid; k < nk; k += ATT_THREADS) pr[k] = pr[k] * inv;
   __syncthreads();
-  if (prof && h == 0 && tid == 0) prof[3] = __builtin_amdgcn_s_memtime();
   // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f (product and sum
   // rounded separately), thread j < c for column dd = c0 + j.  Every thread loads V tiles
   // (KT keys x c floats, float4 per slot) three tiles ahead into registers and stores them
@@ -215,7 +209,6 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm, u
     const bool ok = wid * 64 + (lane & ~31) < c;
     quantize_half<CO>(y, lane, ok, A.oq_qs + (size_t)blk * 16, A.oq_d + blk, A.oxd + (size_t)blk * QK);
   }
-  if (prof && h == 0 && tid == 0) prof[4] = __builtin_amdgcn_s_memtime();
 }
 
 }  // namespace vsim

@@ -258,13 +258,6 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
 size_t attn_prefill_scratch(int E, int nk);
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
                       hipStream_t s);
-// One exact decode layer (gemv_chain.hip, k_layer_exact): ln = its n_ln LayerNorm jobs
-// (n_ln = 0: the norm ran before), in = fc_in (GELU epilogue), f = fc_out, q = {Q, K, V},
-// o = out-projection; cnt: four counters at cnt[0], [64], [128], [192], zeroed before the
-// launch.  in.nj == 0: fc_in ran before (then n_ln must be 0).
-int launch_layer_exact(const LnQuantJob *ln, int n_ln, const GemvBatch &in, const GemvBatch &f, const GemvBatch &q,
-                       const GemvBatch &o, const AttnJob &a, unsigned *cnt, int n_ctx, int fsolo, int qfirst,
-                       hipStream_t s);
 int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
 int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s,

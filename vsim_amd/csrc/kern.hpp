@@ -161,15 +161,10 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
                                const float *__restrict__ gb, unsigned *stats, const float *__restrict__ ja = nullptr,
                                const float *__restrict__ jab = nullptr, const float *__restrict__ jf = nullptr,
                                const float *__restrict__ jfb = nullptr, float *__restrict__ jout = nullptr,
-                               unsigned long long *prof = nullptr, int s0 = 0, int s1 = 1 << 30) {
+                               int s0 = 0, int s1 = 1 << 30) {
   // [s0, s1): the float4 slice of the row this workgroup normalizes (and writes to jout);
   // the statistics always cover the whole row
   constexpr int NW = NT / 64;
-  // timing experiment (prof != null): phase stamps of thread 0
-  auto stamp = [&](int i) {
-    if (prof && threadIdx.x == 0) prof[i] = __builtin_amdgcn_s_memtime();
-  };
-  stamp(0);
   __shared__ double shs[NW], shsa[NW];
   __shared__ int shu[NW];
   __shared__ double bcast_d;
@@ -228,7 +223,6 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     for (int i = threadIdx.x; i < n4; i += NT)
       join(i, ((const float4 *)x)[i], ld4(ja, i), ld4(jab, i), ld4(jf, i), ld4(jfb, i));
   }
-  stamp(1);
   s = wave_sum_d(s);
   sa = wave_sum_d(sa);
   um = wave_min_i(um);
@@ -266,7 +260,6 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     s = bcast_d;
   }
   const double mean = s / n;
-  stamp(2);
   double s2 = 0.0;
   for (int i = threadIdx.x; i < n4; i += NT) {
     const float4 v4 = ((const float4 *)row)[i];
@@ -284,7 +277,6 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   s2 = 0.0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) s2 += shs[w];
-  stamp(3);
   const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
   const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
   const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
@@ -302,7 +294,6 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     __syncthreads();
     scale = bcast_f;
   }
-  stamp(4);
   for (int i = max(s0, 0) + (int)threadIdx.x; i < min(s1, n4); i += NT) {
     const float4 v4 = ((const float4 *)row)[i];
     float e[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -322,7 +313,6 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     ((float4 *)row)[i] = make_float4(e[0], e[1], e[2], e[3]);
   }
   __syncthreads();
-  stamp(5);
 }
 
 __device__ __forceinline__ void ln_exact_lds(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,

@@ -1,16 +1,17 @@
 // vsim_amd/csrc/layer.hip — fused kernels of the single-token decode step.
 //
-// One decoder layer = 4 launches (vsim.cpp:521-696 for GPT-NeoX with parallel residual,
-// the same ops for GPT-J):
-//   1. k_ln_quant      LayerNorm(s) + affine + activation quantization (ggml.c:4246,
-//                      5024-5041): inpL -> Q4_0 activation row(s) and their xd factors
-//   2. GEMV batch      {Q, K, V, fc_in} in one launch; fc_in's epilogue adds the bias, looks
+// One decoder layer (vsim.cpp:521-696 for GPT-NeoX with parallel residual, the same ops for
+// GPT-J) = 3 launches in exact mode:
+//   1. k_ln_quant      (the previous layer's residual join +) LayerNorm(s) + affine +
+//                      activation quantization (ggml.c:4246, 5024-5041): inpL -> Q4_0
+//                      activation row(s) and their xd factors
+//   2. GEMV batch      {fc_in, Q, K, V} in one launch; fc_in's epilogue adds the bias, looks
 //                      up GELU and quantizes each 32-row tile into the fc_out activation
-//   3. k_attn_decode   per head: RoPE on q and the new k, KV-cache write, KQ (double
-//                      accumulator), scale/softmax (fp16 exp table), KQV (sequential float
-//                      mad), quantize the head's output for the out-projection
-//   4. dual GEMV       out-projection and fc_out for the same 32 rows in one workgroup,
-//                      epilogue inpL += (attn + ff)  (vsim.cpp:694-695)
+//   3. k_layer_tail    (gemv_chain.hip) fc_out beside the attention heads (attn.hpp: RoPE,
+//                      KV-cache write, KQ with a double accumulator, scale/softmax with the
+//                      fp16 exp table, KQV as a sequential float chain, quantization) and the
+//                      out-projection; k_attn_decode below is the same head as its own launch
+//                      for contexts whose scores do not fit the tail's LDS
 // Every value is computed with the reference's operation order and rounding (exact mode);
 // the fast mode swaps in the integer-dot GEMV bodies.  n_past is read from device memory so
 // the whole step can be captured once in a hipGraph and replayed per token.
@@ -28,41 +29,31 @@ extern unsigned *g_norm_stats;
 // One 1024-thread workgroup per LayerNorm (two for GPT-NeoX's parallel-residual pair); the
 // normalized row is quantized by whole waves, two 32-blocks per wave step.
 constexpr int LNQ_THREADS = 512;
-__device__ unsigned long long g_ln_prof[8];  // timing experiment output (VSIM_LN_DBG)
 
 // LNQ_SPLIT workgroups per LayerNorm: each computes the whole row's statistics (the row is
 // 16 KB, read from L2) and normalizes, writes and quantizes one slice of LNQ_SPLIT, so the
 // latency-bound per-element phases run on LNQ_SPLIT CUs.
 constexpr int LNQ_SPLIT = 8;
-template <bool PROF>
 __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float row[];
   const int part = blockIdx.x % LNQ_SPLIT;
   const LnQuantJob &J = blockIdx.x < LNQ_SPLIT ? j0 : j1;
-  unsigned long long *prof = PROF && blockIdx.x == 0 ? g_ln_prof : nullptr;
   if (J.clear && blockIdx.x == 0 && threadIdx.x < 3) J.clear[64 * threadIdx.x] = 0u;
   const int nb = n / QK, lane = threadIdx.x & 63;
   const int b0 = part * nb / LNQ_SPLIT, b1 = (part + 1) * nb / LNQ_SPLIT;  // this slice's blocks
   ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, part == 0 ? stats : nullptr, J.ja, J.jab, J.jf, J.jfb, J.jout,
-                              prof, b0 * QK / 4, b1 * QK / 4);
+                              b0 * QK / 4, b1 * QK / 4);
   for (int b2 = threadIdx.x >> 6; b0 + 2 * b2 < b1; b2 += LNQ_THREADS / 64) {
     const int b = b0 + 2 * b2 + (lane >> 5);
     const bool ok = b < b1;
     const float v = ok ? row[b * QK + (lane & 31)] : 0.0f;
     quantize_half(v, lane, ok, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
   }
-  if (PROF && blockIdx.x == 0 && threadIdx.x == 0) g_ln_prof[6] = __builtin_amdgcn_s_memtime();
 }
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
-  static const bool prof = getenv("VSIM_LN_DBG") != nullptr;
   const dim3 grid((j1 ? 2 : 1) * LNQ_SPLIT);
-  if (prof)
-    hipLaunchKernelGGL(k_ln_quant<true>, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
-                       g_norm_stats);
-  else
-    hipLaunchKernelGGL(k_ln_quant<false>, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n,
-                       g_norm_stats);
+  hipLaunchKernelGGL(k_ln_quant, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n, g_norm_stats);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -147,11 +138,9 @@ int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s) {
 // ------------------------------------------------------------------ 3. attention (N = 1)
 // attn.hpp; one 1024-thread workgroup per head
 constexpr int ATT_THREADS = 1024;
-__device__ unsigned long long g_attn_prof[8];  // timing experiment output (VSIM_ATT_DBG)
-template <bool PROF>
 __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(AttnJob A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  attn_body<ATT_THREADS>(A, blockIdx.x, sm, PROF ? g_attn_prof : nullptr);
+  attn_body<ATT_THREADS>(A, blockIdx.x, sm);
 }
 
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s) {
@@ -161,19 +150,9 @@ int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s) {
     return VSIM_EINVAL;
   }
   const size_t smem = (size_t)attn_lds_floats(A.d, n_ctx) * sizeof(float);
-  static const bool prof = getenv("VSIM_ATT_DBG") != nullptr;
-  if (prof) hipLaunchKernelGGL(k_attn_decode<true>, dim3(A.H * S), dim3(ATT_THREADS), smem, s, A);
-  else hipLaunchKernelGGL(k_attn_decode<false>, dim3(A.H * S), dim3(ATT_THREADS), smem, s, A);
+  hipLaunchKernelGGL(k_attn_decode, dim3(A.H * S), dim3(ATT_THREADS), smem, s, A);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
 
 }  // namespace vsim
-
-extern "C" int vsim_debug_attn_prof(unsigned long long *out8) {
-  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(vsim::g_attn_prof), sizeof(vsim::g_attn_prof)) == hipSuccess ? 0 : -1;
-}
-
-extern "C" int vsim_debug_ln_prof(unsigned long long *out8) {
-  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(vsim::g_ln_prof), sizeof(vsim::g_ln_prof)) == hipSuccess ? 0 : -1;
-}

@@ -103,19 +103,27 @@ struct vsim_model {
   void *pf_x16 = nullptr;      // fast prefill: fp16 GEMM operands, [n_max][E] then [n_max][4E]
   size_t pf_bytes = 0;
 
-  // second decode stream: the attention branch (Q/K/V, attention, out-projection) runs beside
-  // fc_out, whose K = 4E chain is the layer's critical path
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int graph_mode = -1;
   int graph_kernels = 0;
 
-  // GEMV profiling (bench.py's live roofline): event pair around every GEMV launch
+  // Per-kernel profiling (bench.py's live roofline): with profiling on, the decode step runs
+  // eagerly and an event pair brackets every launch, tagged with the kernel's name and the
+  // algorithmic bytes it moves (Q4_0 weights at 0.625 B/weight, KV rows, activations).
+  struct ProfRec {
+    size_t ev;
+    const char *kind;
+    double bytes;
+  };
+  struct ProfKind {
+    std::string name;
+    double ms = 0.0, bytes = 0.0;
+    long n = 0;
+  };
   bool profile = false;
   std::vector<hipEvent_t> prof_events;
+  std::vector<ProfRec> prof_pending;
   size_t prof_used = 0;
-  double prof_ms = 0.0, prof_bytes = 0.0;
-  long prof_launches = 0;
+  std::vector<ProfKind> prof_kinds;
 };
 
 namespace {
@@ -409,6 +417,48 @@ void bind_pointers(vsim_model *m) {
     if (rc_) return rc_;         \
   } while (0)
 
+// Profiling brackets (eager launches only): prof_begin records the start event and returns
+// its slot (-1 when profiling is off); prof_end records the end and tags the pair.
+long prof_begin(vsim_model *m) {
+  if (!m->profile) return -1;
+  if (m->prof_used + 2 > m->prof_events.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
+    m->prof_events.push_back(a);
+    m->prof_events.push_back(b);
+  }
+  const size_t i = m->prof_used;
+  m->prof_used += 2;
+  (void)hipEventRecord(m->prof_events[i], m->stream);
+  return (long)i;
+}
+void prof_end(vsim_model *m, long ev, const char *kind, double bytes) {
+  if (ev < 0) return;
+  (void)hipEventRecord(m->prof_events[ev + 1], m->stream);
+  m->prof_pending.push_back({(size_t)ev, kind, bytes});
+}
+// after the stream synchronised: fold the pending pairs into the per-kernel totals
+int prof_collect(vsim_model *m) {
+  for (const auto &r : m->prof_pending) {
+    float ms = 0.0f;
+    VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[r.ev], m->prof_events[r.ev + 1]));
+    size_t k = 0;
+    while (k < m->prof_kinds.size() && m->prof_kinds[k].name != r.kind) ++k;
+    if (k == m->prof_kinds.size()) {
+      m->prof_kinds.emplace_back();
+      m->prof_kinds.back().name = r.kind;
+    }
+    m->prof_kinds[k].ms += ms;
+    m->prof_kinds[k].bytes += r.bytes;
+    m->prof_kinds[k].n += 1;
+  }
+  m->prof_pending.clear();
+  m->prof_used = 0;
+  return VSIM_OK;
+}
+
+double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
+
 // Quantize an activation and run one GEMV in the model's mode.  x16 non-null (fast-mode
 // prompt batches): the activation is already the GEMM's fp16 operand (launch_act_quant_f16).
 int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_t *xq, float *xd, bool quantize,
@@ -417,28 +467,14 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
     RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
     ++nk;
   }
-  hipEvent_t *ev = nullptr;
-  if (m->profile) {
-    if (m->prof_used + 2 > m->prof_events.size()) {
-      hipEvent_t a, b;
-      VSIM_HIP(hipEventCreate(&a));
-      VSIM_HIP(hipEventCreate(&b));
-      m->prof_events.push_back(a);
-      m->prof_events.push_back(b);
-    }
-    ev = &m->prof_events[m->prof_used];
-    m->prof_used += 2;
-    VSIM_HIP(hipEventRecord(ev[0], m->stream));
-  }
+  const long ev = prof_begin(m);
   if (x16) {
     RC(launch_gemm_f16x(w4_view(W, M, K), x16, N, bias, y, m->stream));
   } else {
     RC(launch_q4_gemv(W, M, K, xq, xd, N, bias, y, m->mode, m->stream));
   }
-  if (ev) {
-    VSIM_HIP(hipEventRecord(ev[1], m->stream));
-    m->prof_bytes += (double)M * K / QK * QBYTES;
-  }
+  prof_end(m, ev, x16 ? "k_gemm_f16 (prompt)" : N > 1 ? "gemv (prompt rows)" : "gemv (general path)",
+           (double)M * K / QK * QBYTES);
   ++nk;
   return VSIM_OK;
 }
@@ -492,12 +528,6 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   return VSIM_OK;
 }
 
-static int env_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e && e[0] ? atoi(e) : dflt;
-}
-
-
 int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   if (m->arch == VSIM_ARCH_BLOOM) return run_layer_bloom(m, il, n_past, N, nk);
   const LayerW &L = m->layers[il - m->l0];
@@ -508,8 +538,7 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // (quantize_row_q4_0 values, k_act_quant_f16; the GELU folded into fc_out's)
   // (operands in the model's scratch, pf_x16: [N][E] norm outputs, then [N][F] attention /
   // GELU outputs)
-  static const int pf_env = env_int("VSIM_PF_ACT", 1);  // 0: per-GEMM quantize + dequant (A/B)
-  const bool pf = pf_env && m->mode == VSIM_MODE_FAST && N >= GEMM_MIN_N && m->pf_x16;
+  const bool pf = m->mode == VSIM_MODE_FAST && N >= GEMM_MIN_N && m->pf_x16;
   struct {
     void *a, *b;
   } X = {m->pf_x16, pf ? (void *)((uint16_t *)m->pf_x16 + (size_t)N * E) : nullptr};
@@ -533,8 +562,7 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
-  static const int pfa_env = env_int("VSIM_PF_ATT", 1);  // 0: the per-op attention (A/B)
-  if (pfa_env && m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
+  if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
     // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
     if (!m->pf_scratch) {  // (prompt evals are never graph-captured: allocating here is safe)
       m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
@@ -580,67 +608,16 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   return VSIM_OK;
 }
 
-// GEMV profiling brackets (eager launches only; bench.py's live roofline)
-hipEvent_t *prof_begin(vsim_model *m, hipStream_t st = nullptr) {
-  if (!m->profile) return nullptr;
-  if (m->prof_used + 2 > m->prof_events.size()) {
-    hipEvent_t a, b;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return nullptr;
-    m->prof_events.push_back(a);
-    m->prof_events.push_back(b);
-  }
-  hipEvent_t *ev = &m->prof_events[m->prof_used];
-  m->prof_used += 2;
-  (void)hipEventRecord(ev[0], st ? st : m->stream);
-  return ev;
-}
-void prof_end(vsim_model *m, hipEvent_t *ev, double bytes, hipStream_t st = nullptr) {
-  if (!ev) return;
-  (void)hipEventRecord(ev[1], st ? st : m->stream);
-  m->prof_bytes += bytes;
-}
-
-double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
-
 // Fast-mode single-token step (fast_decode.hip): 3 launches per layer.  Same buffers and
 // the same replayable form as enqueue_decode (token and n_past from device memory).
 // Shapes the fast step handles: head dim a multiple of 32 up to 256, rotary pairs inside one
 // 32-row tile (GPT-J pairs; GPT-NeoX rotate-half with n_rot <= 32), n_embd <= 8192.
-// fc_out K splits: FD_SF (or VSIM_FAST_SF = 1, 2, 4 or 8; A/B timing), doubled until one
-// split's activation slice fits the LDS staging (at most FD_MAXE values)
+// fc_out K splits: FD_SF, doubled until one split's activation slice fits the LDS staging
+// (at most FD_MAXE values)
 int fast_sf(const vsim_model *m) {
-  static const int sf0 = [] {
-    const char *e = getenv("VSIM_FAST_SF");
-    const int v = e ? atoi(e) : FD_SF;
-    return v == 1 || v == 2 || v == 4 || v == 8 ? v : FD_SF;
-  }();
-  int sf = sf0;
+  int sf = FD_SF;
   while (sf < 8 && 4 * m->hp.n_embd / sf > FD_MAXE) sf *= 2;
   return sf;
-}
-
-// VSIM_LAYER=1|2 select the one-launch layer kernel (k_layer_exact; 2: fc_in as a launch of
-// its own before it).  Bit-identical to the default three-launch layer, but not faster on
-// GPT-J-6B (489 vs 510 tok/s), so 0 is the default.
-int layer_mode() {
-  static const int v = env_int("VSIM_LAYER", 0);
-  return v;
-}
-int lx_fsolo() {  // VSIM_LX_FSOLO=0: fc_out as 32-row tiles inside k_layer_exact
-  static const int v = env_int("VSIM_LX_FSOLO", 1);
-  return v;
-}
-int lx_qfirst() {  // VSIM_LX_QFIRST=1: Q/K/V before fc_out in the grid
-  static const int v = env_int("VSIM_LX_QFIRST", 0);
-  return v;
-}
-
-bool fast_ln_fused() {
-  static const bool v = [] {
-    const char *e = getenv("VSIM_FAST_LN");
-    return !(e && e[0] == '0');
-  }();
-  return v;
 }
 
 bool fast_decode_ok(const vsim_model *m) {
@@ -657,8 +634,8 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
   DevTables tab;
   RC(tables_get(&tab));
   const int nbE = E / QK, nbF = F / QK;
-  uint8_t *q1 = m->xq1, *q2 = m->xq2, *q3 = m->xq3;
-  float *d1 = (float *)(q1 + (size_t)nbE * 16), *d2 = (float *)(q2 + (size_t)nbE * 16);
+  uint8_t *q1 = m->xq1, *q3 = m->xq3;
+  float *d1 = (float *)(q1 + (size_t)nbE * 16), *d2 = (float *)(m->xq2 + (size_t)nbE * 16);
   float *d3 = (float *)(q3 + (size_t)nbF * 16);
   if (m->first) {
     RC(launch_get_rows(m->wte, E, V, m->tok_dev, 1, m->inpL, s));
@@ -666,40 +643,23 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
   }
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
   const int nchunk = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
+  const double kv_bytes = 2.0 * ((double)m->npast_host[0] + 1) * E * sizeof(float);
   float *R[2] = {m->inpL, m->inpL2};
   int cur = 0;
   for (int il = m->l0; il < m->l1; ++il) {
     const LayerW &L = m->layers[il - m->l0];
     const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
-    // LayerNorm(s) -> Q4 activations (GPT-J: one LayerNorm feeds attention and MLP): in
-    // the GEMV's prologue (VSIM_FAST_LN=0: a separate k_fast_ln launch)
+    // LayerNorm(s) -> Q4 activations in the GEMV's prologue (GPT-J: one LayerNorm feeds
+    // attention and MLP), then {fc_in -> GELU -> quantize, Q, K, V}
     FastGemv P{};
-    if (fast_ln_fused()) {
-      P.lnx = R[cur];
-      P.lnw[0] = L.ln1_w;
-      P.lnb[0] = L.ln1_b;
-      P.lnw[1] = gptj ? L.ln1_w : L.ln2_w;
-      P.lnb[1] = gptj ? L.ln1_b : L.ln2_b;
-    } else {
-      FastLn N{};
-      N.x = R[cur];
-      N.E = E;
-      N.n = gptj ? 1 : 2;
-      N.w[0] = L.ln1_w;
-      N.b[0] = L.ln1_b;
-      N.w[1] = L.ln2_w;
-      N.b[1] = L.ln2_b;
-      N.qs[0] = q1;
-      N.d[0] = d1;
-      N.qs[1] = q2;
-      N.d[1] = d2;
-      RC(launch_fast_ln(N, s));
-      ++nk;
-    }
-    // {fc_in -> GELU -> quantize, Q, K, V}
+    P.lnx = R[cur];
+    P.lnw[0] = L.ln1_w;
+    P.lnb[0] = L.ln1_b;
+    P.lnw[1] = gptj ? L.ln1_w : L.ln2_w;
+    P.lnb[1] = gptj ? L.ln1_b : L.ln2_b;
     P.xq[0] = q1;
     P.xd[0] = d1;
-    P.xq[1] = gptj ? q1 : q2;
+    P.xq[1] = gptj ? q1 : m->xq2;
     P.xd[1] = gptj ? d1 : d2;
     P.nj = 4;
     P.j[0] = FastJob{w4_view(L.wfc, F, E), L.bfc, nullptr, FE_GELU_Q, 1};
@@ -716,9 +676,9 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     P.d = d;
     P.n_rot = m->hp.n_rot;
     P.style = gptj ? 1 : 0;
-    hipEvent_t *ev = prof_begin(m);
+    long ev = prof_begin(m);
     RC(launch_fast_gemv(P, E, s));
-    prof_end(m, ev, w4_algo_bytes(P.j[0].w) + 3 * w4_algo_bytes(P.j[1].w));
+    prof_end(m, ev, "k_fast_gemv (fc_in, Q, K, V)", w4_algo_bytes(P.j[0].w) + 3 * w4_algo_bytes(P.j[1].w));
     ++nk;
     // fc_out split over K | attention chunks
     FastTail T{};
@@ -753,68 +713,47 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
     O.out = R[cur ^ 1];
     ev = prof_begin(m);
     RC(launch_fast_tail(T, s));
-    prof_end(m, ev, w4_algo_bytes(T.wf));
+    prof_end(m, ev, "k_fast_tail (fc_out + attention)", w4_algo_bytes(T.wf) + kv_bytes);
     ++nk;
     ev = prof_begin(m);
     RC(launch_fast_oproj_join(O, s));
-    prof_end(m, ev, w4_algo_bytes(O.w));
+    prof_end(m, ev, "k_fast_oproj_join", w4_algo_bytes(O.w));
     ++nk;
     cur ^= 1;
   }
   if (m->last) {
     FastGemv P{};
-    if (fast_ln_fused()) {
-      P.lnx = R[cur];
-      P.lnw[0] = P.lnw[1] = m->lnf_w;
-      P.lnb[0] = P.lnb[1] = m->lnf_b;
-    } else {
-      FastLn N{};
-      N.x = R[cur];
-      N.E = E;
-      N.n = 1;
-      N.w[0] = m->lnf_w;
-      N.b[0] = m->lnf_b;
-      N.qs[0] = q1;
-      N.d[0] = d1;
-      RC(launch_fast_ln(N, s));
-      ++nk;
-    }
+    P.lnx = R[cur];
+    P.lnw[0] = P.lnw[1] = m->lnf_w;
+    P.lnb[0] = P.lnb[1] = m->lnf_b;
     P.xq[0] = P.xq[1] = q1;
     P.xd[0] = P.xd[1] = d1;
     P.nj = 1;
     P.j[0] = FastJob{w4_view(m->lmh, V, E), gptj ? m->lmh_b : nullptr, m->logits, FE_STORE, 0};
-    hipEvent_t *ev = prof_begin(m);
+    const long ev = prof_begin(m);
     RC(launch_fast_gemv(P, E, s));
-    prof_end(m, ev, w4_algo_bytes(P.j[0].w));
+    prof_end(m, ev, "k_fast_gemv (lm_head)", w4_algo_bytes(P.j[0].w));
     ++nk;
   }
   m->resid_final = R[cur];
   return VSIM_OK;
 }
 
-// The single-token decode step as 4 fused launches per layer (layer.hip).  Reads the token
-// from tok_dev and n_past from npast_dev, so the enqueued sequence is replayable.
+// Exact mode: the single-token decode step as 3 fused launches per layer (layer.hip,
+// gemv_chain.hip).  Reads the token from tok_dev and n_past from npast_dev, so the enqueued
+// sequence is replayable (hipGraph).
+//   1. k_ln_quant: (join of the previous layer +) input LayerNorm (+ post_attention
+//      LayerNorm for GPT-NeoX), quantized
+//   2. k_gemv_solo: {fc_in (+ bias, GELU, requantize), Q, K, V}
+//   3. k_layer_tail: fc_out beside the attention heads and the out-projection; no biases
+//      (they join in the next layer's step 1)
+// fc_out's K = 4E chain (vsim.cpp:680-690) is the layer's longest dependency, so the
+// attention branch fills the CUs beside it instead of running before it.
 int enqueue_decode(vsim_model *m, int &nk) {
-  static const bool fast_env = [] {  // VSIM_FAST_DECODE=0: fast mode on the older kernels
-    const char *e = getenv("VSIM_FAST_DECODE");
-    return !(e && e[0] == '0');
-  }();
-  if (m->mode == VSIM_MODE_FAST && fast_env && fast_decode_ok(m)) return enqueue_decode_fast(m, nk);
+  if (m->mode == VSIM_MODE_FAST && fast_decode_ok(m)) return enqueue_decode_fast(m, nk);
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
   const bool gptj = m->arch == VSIM_ARCH_GPTJ;
   hipStream_t s = m->stream;
-  // fc_out, attention and out-projection as one launch (k_layer_tail); VSIM_TAIL=0: separate
-  static const bool tail_env = [] {
-    const char *e = getenv("VSIM_TAIL");
-    return !(e && e[0] == '0');
-  }();
-  // VSIM_SPLIT=1: the attention branch on a second stream beside fc_out.  Measured slower
-  // (413 vs 442 tok/s, GPT-J): each cross-queue event wait costs 4-10 us, more than the
-  // overlap wins.  Kept for A/B timing.
-  static const bool split = [] {
-    const char *e = getenv("VSIM_SPLIT");
-    return e && e[0] == '1';
-  }();
   DevTables tab;
   RC(tables_get(&tab));
   const int nbE = E / QK, nbF = F / QK;
@@ -826,6 +765,14 @@ int enqueue_decode(vsim_model *m, int &nk) {
     ++nk;
   }
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  // algorithmic bytes of the profiled launches: KV rows read (P + 1) and
+  // written by the attention, rows of E floats read / written by the LayerNorm step
+  const double kv_bytes = 2.0 * ((double)m->npast_host[0] + 1) * E * sizeof(float);
+  // reads: the row (+ the four join vectors), each norm's affine; writes: the joined row, each
+  // norm's factors xd (E floats) and Q4 row (0.625 B per value)
+  auto ln_bytes = [&](int nnorm, bool join) {
+    return 4.0 * E * (1 + (join ? 5 : 0) + 3 * nnorm) + 0.625 * E * nnorm;
+  };
   // The residual join of layer l (inpL += attn + ff, vsim.cpp:694-695) runs inside layer
   // l+1's LayerNorm kernel (or the final norm); the joined row goes to the other of the two
   // residual buffers, so both norm workgroups of GPT-NeoX can read the old one.
@@ -840,85 +787,53 @@ int enqueue_decode(vsim_model *m, int &nk) {
     j.jfb = pend_fb;
     j.jout = write ? R[cur ^ 1] : nullptr;
   };
+  auto job = [&](GemvBatch &Bt, int i, void *W, int M, int K, const float *xd, const uint8_t *xq, const float *xdd,
+                 const float *bias, float *y) {
+    GemvJob &J = Bt.j[i];
+    J.w = w4_view(W, M, K);
+    J.xd = xd;
+    J.xqs = xq;
+    J.xdd = xdd;
+    J.bias = bias;
+    J.y = y;
+    J.epi = EPI_STORE;
+  };
+  // the attention heads fuse into k_layer_tail while their LDS (scores over n_ctx) fits it
+  const bool tail = m->mode == VSIM_MODE_EXACT && (size_t)attn_lds_floats(d, m->n_ctx) * sizeof(float) <= 75264;
   for (int il = m->l0; il < m->l1; ++il) {
     const LayerW &L = m->layers[il - m->l0];
     const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
-    // 1. (join of the previous layer +) input LayerNorm (+ post_attention LayerNorm for
-    //    GPT-NeoX), quantized
+    // 1. (join +) LayerNorm(s) + quantize
     LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
     LnQuantJob j2{R[cur], L.ln2_w, L.ln2_b, q2, d2, m->xd2};
     if (pending) {
       join_into(j1, true);
       join_into(j2, false);
     }
-    const bool tail = tail_env && !split && m->mode == VSIM_MODE_EXACT &&
-                      (size_t)attn_lds_floats(d, m->n_ctx) * sizeof(float) <= 75264;
-    // VSIM_LAYER: 0 (default) the norm, {fc_in, Q, K, V}, then k_layer_tail; 1 the norm
-    // and everything after it in one launch (k_layer_exact); 2 the norm, fc_in, then the
-    // rest in one launch
-    const int lx = tail ? layer_mode() : 0;
-    unsigned *cnt = m->tail_done + (size_t)(lx ? il - m->l0 : 0) * 256;
-    if (lx && il == m->l0) {
-      VSIM_HIP(hipMemsetAsync(m->tail_done, 0, (size_t)(m->l1 - m->l0) * 256 * sizeof(unsigned), s));
-    }
-    const LnQuantJob lnj[2] = {j1, j2};
-    if (lx != 1) {
-      if (tail) j1.clear = m->tail_done;
-      RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
-      ++nk;
-    }
+    if (tail) j1.clear = m->tail_done;
+    long ev = prof_begin(m);
+    RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
+    prof_end(m, ev, "k_ln_quant", ln_bytes(gptj ? 1 : 2, pending));
+    ++nk;
     if (pending) cur ^= 1;
-    // 2. fc_in (+bias, GELU, requantize) -> 3. fc_out; beside it, on the second stream,
-    //    Q/K/V -> attention -> out-projection.  fc_out's K = 4E chain (vsim.cpp:680-690) is
-    //    the longest dependency of the layer, so fc_in runs alone first (all CUs) and the
-    //    attention branch fills the CUs fc_out leaves idle.  Without split streams the same
-    //    work goes as two batches {fc_in, Q, K, V}, attention, {fc_out, out-proj}.
-    auto job = [&](GemvBatch &Bt, int i, void *W, int M, int K, const float *xd, const uint8_t *xq, const float *xdd,
-                   const float *bias, float *y) {
-      GemvJob &J = Bt.j[i];
-      J.w = w4_view(W, M, K);
-      J.xd = xd;
-      J.xqs = xq;
-      J.xdd = xdd;
-      J.bias = bias;
-      J.y = y;
-      J.epi = EPI_STORE;
-    };
+    // 2. {fc_in (+bias, GELU, requantize), Q, K, V}
     GemvBatch B{};
-    B.nj = split ? 1 : 4;
+    B.nj = 4;
     job(B, 0, L.wfc, F, E, gptj ? m->xd1 : m->xd2, gptj ? q1 : q2, gptj ? d1 : d2, L.bfc, nullptr);
     B.j[0].epi = EPI_GELU_Q;
     B.j[0].gelu_tab = tab.gelu_f16;
     B.j[0].oq_qs = q3;
     B.j[0].oq_d = d3;
     B.j[0].oxd = m->xd3;
-    GemvBatch Bq{};
-    GemvBatch &BQ = split ? Bq : B;
-    const int q0 = split ? 0 : 1;
-    BQ.nj = split ? 3 : 4;
-    job(BQ, q0 + 0, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
-    job(BQ, q0 + 1, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
-    job(BQ, q0 + 2, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
-    hipEvent_t *ev = nullptr;
-    if (lx != 1) {
-      GemvBatch Bi = B;
-      if (lx == 2) Bi.nj = 1;
-      ev = prof_begin(m);
-      RC(launch_gemv_epi(Bi, m->mode, s));
-      prof_end(m, ev, Bi.nj == 1 ? w4_algo_bytes(Bi.j[0].w) : w4_algo_bytes(Bi.j[0].w) + 3 * w4_algo_bytes(Bi.j[1].w));
-      ++nk;
-    }
-    hipStream_t sa = s;  // attention branch
-    if (split) {
-      sa = m->stream2;
-      VSIM_HIP(hipEventRecord(m->ev_fork, s));
-      VSIM_HIP(hipStreamWaitEvent(sa, m->ev_fork, 0));
-      ev = prof_begin(m, sa);
-      RC(launch_gemv_epi(BQ, m->mode, sa));
-      prof_end(m, ev, 3 * w4_algo_bytes(BQ.j[0].w), sa);
-      ++nk;
-    }
-    // attention for the new token
+    job(B, 1, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
+    job(B, 2, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
+    job(B, 3, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
+    ev = prof_begin(m);
+    RC(launch_gemv_epi(B, m->mode, s));
+    prof_end(m, ev, m->mode == VSIM_MODE_EXACT ? "k_gemv_solo (fc_in, Q, K, V)" : "k_gemv_fast_epi (fc_in, Q, K, V)",
+             w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
+    ++nk;
+    // 3. attention for the new token (attn.hpp), fc_out and the out-projection
     AttnJob A{};
     A.q = m->Qb;
     A.k = m->Kb;
@@ -933,71 +848,36 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.n_rot = m->hp.n_rot;
     A.style = gptj ? 1 : 0;
     A.n_ctx = m->n_ctx;
-    // column parts per head (attn.hpp); VSIM_ATT_SPLIT overrides (A/B timing)
-    {
-      static const int split_env = [] {
-        const char *e = getenv("VSIM_ATT_SPLIT");
-        return e ? atoi(e) : 0;
-      }();
-      int S = split_env > 0 ? split_env : 1;
-      while (S > 1 && (d % S != 0 || (d / S) % QK != 0)) --S;
-      A.nsplit = S;
-    }
+    A.nsplit = 1;
     A.scale = scale;
     A.oq_qs = qa;
     A.oq_d = da;
     A.oxd = m->xda;
     A.out = nullptr;
+    GemvBatch Bf{}, Bo{};
+    Bf.nj = 1;
+    job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
+    Bo.nj = 1;
+    job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
     if (tail) {
-      GemvBatch Bf{}, Bo{};
-      Bf.nj = 1;
-      job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
-      Bo.nj = 1;
-      job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
-      if (lx) {
-        GemvBatch Bi{}, Bq{};
-        Bi.nj = lx == 1 ? 1 : 0;
-        Bi.j[0] = B.j[0];
-        Bq.nj = 3;
-        for (int i = 0; i < 3; ++i) Bq.j[i] = B.j[1 + i];
-        ev = prof_begin(m);
-        RC(launch_layer_exact(lnj, lx == 1 ? (gptj ? 1 : 2) : 0, Bi, Bf, Bq, Bo, A, cnt, m->n_ctx, lx_fsolo(),
-                              lx_qfirst(), s));
-        prof_end(m, ev, (lx == 1 ? w4_algo_bytes(B.j[0].w) : 0) + 3 * w4_algo_bytes(B.j[1].w) +
-                            w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w));
-      } else {
-        ev = prof_begin(m);
-        RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
-        prof_end(m, ev, w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w));
-      }
+      ev = prof_begin(m);
+      RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
+      prof_end(m, ev, "k_layer_tail (fc_out + attention + out-proj)",
+               w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + kv_bytes);
       ++nk;
-      pending = true;
-      pend_ab = gptj ? nullptr : L.bo;
-      pend_fb = L.bproj;
-      continue;
-    }
-    RC(launch_attn_decode(A, m->n_ctx, sa));
-    ++nk;
-    // {fc_out, out-projection} without biases (they join in the next norm)
-    GemvBatch B2{};
-    B2.nj = split ? 1 : 2;
-    job(B2, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
-    GemvBatch Bo{};
-    GemvBatch &BO = split ? Bo : B2;
-    BO.nj = split ? 1 : 2;
-    job(BO, split ? 0 : 1, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
-    if (split) {
-      ev = prof_begin(m, sa);
-      RC(launch_gemv_epi(BO, m->mode, sa));
-      prof_end(m, ev, w4_algo_bytes(BO.j[0].w), sa);
+    } else {
+      ev = prof_begin(m);
+      RC(launch_attn_decode(A, m->n_ctx, s));
+      prof_end(m, ev, "k_attn_decode", kv_bytes);
       ++nk;
-      VSIM_HIP(hipEventRecord(m->ev_join, sa));
+      Bf.j[1] = Bo.j[0];
+      Bf.nj = 2;
+      ev = prof_begin(m);
+      RC(launch_gemv_epi(Bf, m->mode, s));
+      prof_end(m, ev, m->mode == VSIM_MODE_EXACT ? "k_gemv_chain32 (fc_out, out-proj)" : "k_gemv_fast_epi (fc_out, out-proj)",
+               w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bf.j[1].w));
+      ++nk;
     }
-    ev = prof_begin(m);
-    RC(launch_gemv_epi(B2, m->mode, s));
-    prof_end(m, ev, split ? w4_algo_bytes(B2.j[0].w) : w4_algo_bytes(B2.j[0].w) + w4_algo_bytes(B2.j[1].w));
-    ++nk;
-    if (split) VSIM_HIP(hipStreamWaitEvent(s, m->ev_join, 0));
     pending = true;
     pend_ab = gptj ? nullptr : L.bo;
     pend_fb = L.bproj;
@@ -1005,21 +885,18 @@ int enqueue_decode(vsim_model *m, int &nk) {
   if (m->last) {
     LnQuantJob jf{R[cur], m->lnf_w, m->lnf_b, q1, d1, m->xd1};
     if (pending) join_into(jf, true);
+    long ev = prof_begin(m);
     RC(launch_ln_quant(jf, nullptr, E, s));
+    prof_end(m, ev, "k_ln_quant", ln_bytes(1, pending));
     ++nk;
     if (pending) cur ^= 1;
     GemvBatch B{};
     B.nj = 1;
-    B.j[0].w = w4_view(m->lmh, V, E);
-    B.j[0].xd = m->xd1;
-    B.j[0].xqs = q1;
-    B.j[0].xdd = d1;
-    B.j[0].bias = gptj ? m->lmh_b : nullptr;
-    B.j[0].y = m->logits;
-    B.j[0].epi = EPI_STORE;
-    hipEvent_t *ev = prof_begin(m);
+    job(B, 0, m->lmh, V, E, m->xd1, q1, d1, gptj ? m->lmh_b : nullptr, m->logits);
+    ev = prof_begin(m);
     RC(launch_gemv_epi(B, m->mode, s));
-    prof_end(m, ev, w4_algo_bytes(B.j[0].w));
+    prof_end(m, ev, m->mode == VSIM_MODE_EXACT ? "k_gemv_solo (lm_head)" : "k_gemv_fast_epi (lm_head)",
+             w4_algo_bytes(B.j[0].w));
     ++nk;
   } else if (pending) {
     RC(launch_residual_join(R[cur], m->attn, pend_ab, m->ff, pend_fb, R[cur ^ 1], E, s));
@@ -1031,8 +908,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
 }
 
 bool fused_ok(const vsim_model *m, int N) {
-  static const bool disabled = getenv("VSIM_NO_FUSED") != nullptr;
-  return !disabled && N == 1 && (m->arch == VSIM_ARCH_GPTJ || m->hp.use_parallel_residual == 1);
+  return N == 1 && (m->arch == VSIM_ARCH_GPTJ || m->hp.use_parallel_residual == 1);
 }
 
 thread_local std::string t_err;
@@ -1089,10 +965,7 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   m->first = layer_begin == 0;
   m->last = layer_end == hp->n_layer;
   auto fail = [&](int rc) { vsim_model_free(m); return rc; };
-  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming) != hipSuccess)
+  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(hip_fail(hipErrorUnknown, "stream"));
   std::vector<std::pair<std::string, Slot>> plan;
   plan_slots(m, plan);
@@ -1150,9 +1023,7 @@ void vsim_model_free(vsim_model *m) {
   if (m->vcache) (void)hipFree(m->vcache);
   if (m->rope_cs) (void)hipFree(m->rope_cs);
   if (m->stream) (void)hipStreamDestroy(m->stream);
-  if (m->stream2) (void)hipStreamDestroy(m->stream2);
-  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
-  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
+  for (hipEvent_t e : m->prof_events) (void)hipEventDestroy(e);
   delete m;
 }
 
@@ -1185,6 +1056,37 @@ int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, siz
   }
   s.loaded = true;
   return VSIM_OK;
+}
+
+int vsim_model_get_tensor(vsim_model *m, const char *name, void *host, size_t nbytes) {
+  if (!m || !name || !host) { set_error("get_tensor: null argument"); return VSIM_EINVAL; }
+  {  // BLOOM's fused query_key_value weight: the three row blocks back to back
+    const std::string n(name), suf = "attention.query_key_value.weight";
+    if (m->arch == VSIM_ARCH_BLOOM && n.size() >= suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0) {
+      const char *parts[3] = {"/q", "/k", "/v"};
+      if (nbytes % 3 != 0) { set_error("get_tensor: fused qkv size"); return VSIM_EINVAL; }
+      for (int i = 0; i < 3; ++i)
+        RC(vsim_model_get_tensor(m, (n + parts[i]).c_str(), (uint8_t *)host + i * (nbytes / 3), nbytes / 3));
+      return VSIM_OK;
+    }
+  }
+  auto it = m->slots.find(name);
+  if (it == m->slots.end()) { set_error(std::string("get_tensor: unknown tensor ") + name); return VSIM_EINVAL; }
+  const Slot &s = it->second;
+  if (nbytes != slot_bytes(s)) { set_error(std::string("get_tensor: wrong size for ") + name); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  VSIM_HIP(hipStreamSynchronize(m->stream));
+  if (s.kind == KF32) {
+    VSIM_HIP(hipMemcpy(host, s.ptr, nbytes, hipMemcpyDeviceToHost));
+    return VSIM_OK;
+  }
+  void *stage = nullptr;
+  VSIM_HIP(hipMalloc(&stage, nbytes));
+  int rc = launch_q4_unpack(s.ptr, stage, s.rows, s.k, m->stream);
+  if (rc == 0 && hipStreamSynchronize(m->stream) != hipSuccess) rc = hip_fail(hipErrorUnknown, "unpack");
+  if (rc == 0 && hipMemcpy(host, stage, nbytes, hipMemcpyDeviceToHost) != hipSuccess) rc = hip_fail(hipErrorUnknown, "download");
+  (void)hipFree(stage);
+  return rc;
 }
 
 int vsim_model_randomize(vsim_model *m, uint64_t seed, float stddev) {
@@ -1389,15 +1291,7 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
   }
   VSIM_HIP(hipStreamSynchronize(s));
   *next_token = m->am_host[0];
-  if (m->profile) {
-    for (size_t i = 0; i + 1 < m->prof_used; i += 2) {
-      float ms = 0.0f;
-      VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[i], m->prof_events[i + 1]));
-      m->prof_ms += ms;
-      ++m->prof_launches;
-    }
-    m->prof_used = 0;
-  }
+  if (m->profile) RC(prof_collect(m));
   return VSIM_OK;
 }
 
@@ -1428,15 +1322,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   }
   VSIM_HIP(hipMemcpyAsync(tokens_out, m->hist_dev + n_past, sizeof(int32_t) * n_steps, hipMemcpyDeviceToHost, s));
   VSIM_HIP(hipStreamSynchronize(s));
-  if (m->profile) {
-    for (size_t i = 0; i + 1 < m->prof_used; i += 2) {
-      float ms = 0.0f;
-      VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[i], m->prof_events[i + 1]));
-      m->prof_ms += ms;
-      ++m->prof_launches;
-    }
-    m->prof_used = 0;
-  }
+  if (m->profile) RC(prof_collect(m));
   return VSIM_OK;
 }
 
@@ -1510,30 +1396,43 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
   VSIM_HIP(hipStreamSynchronize(s));
   if (m->last && logits) memcpy(logits, m->logit_host, sizeof(float) * V);
   m->kernels_last = nk;
-  if (m->profile) {
-    for (size_t i = 0; i + 1 < m->prof_used; i += 2) {
-      float ms = 0.0f;
-      VSIM_HIP(hipEventElapsedTime(&ms, m->prof_events[i], m->prof_events[i + 1]));
-      m->prof_ms += ms;
-      m->prof_launches++;
-    }
-    m->prof_used = 0;
-  }
+  if (m->profile) RC(prof_collect(m));
   return VSIM_OK;
 }
 
 int vsim_model_set_profile(vsim_model *m, int enable) {
   m->profile = enable != 0;
-  m->prof_ms = m->prof_bytes = 0.0;
-  m->prof_launches = 0;
+  m->prof_kinds.clear();
+  m->prof_pending.clear();
   m->prof_used = 0;
   return VSIM_OK;
 }
 
 int vsim_model_profile_stats(vsim_model *m, double *gemv_ms, long *gemv_launches, double *gemv_bytes) {
-  if (gemv_ms) *gemv_ms = m->prof_ms;
-  if (gemv_launches) *gemv_launches = m->prof_launches;
-  if (gemv_bytes) *gemv_bytes = m->prof_bytes;
+  double ms = 0.0, by = 0.0;
+  long n = 0;
+  for (const auto &k : m->prof_kinds) {
+    ms += k.ms;
+    by += k.bytes;
+    n += k.n;
+  }
+  if (gemv_ms) *gemv_ms = ms;
+  if (gemv_launches) *gemv_launches = n;
+  if (gemv_bytes) *gemv_bytes = by;
+  return VSIM_OK;
+}
+
+int vsim_model_profile_kernel(vsim_model *m, int i, char *name, int name_cap, double *ms, long *launches,
+                              double *bytes) {
+  if (!m || i < 0 || i >= (int)m->prof_kinds.size()) return VSIM_EINVAL;
+  const auto &k = m->prof_kinds[i];
+  if (name && name_cap > 0) {
+    std::strncpy(name, k.name.c_str(), (size_t)name_cap - 1);
+    name[name_cap - 1] = 0;
+  }
+  if (ms) *ms = k.ms;
+  if (launches) *launches = k.n;
+  if (bytes) *bytes = k.bytes;
   return VSIM_OK;
 }
 

@@ -32,11 +32,12 @@ EXPORTS = [
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
     "vsim_op_attn_prefill",
     "vsim_op_tables",
-    "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_randomize",
+    "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_get_tensor",
+    "vsim_model_randomize",
     "vsim_model_set_mode", "vsim_model_hparams", "vsim_model_eval", "vsim_model_eval_argmax", "vsim_model_generate",
     "vsim_model_stream",
     "vsim_model_logits_dev", "vsim_model_info", "vsim_model_set_graph", "vsim_model_set_profile",
-    "vsim_model_profile_stats", "vsim_model_free",
+    "vsim_model_profile_kernel", "vsim_model_profile_stats", "vsim_model_free",
 ]
 
 _lib = None
@@ -81,6 +82,7 @@ def lib():
     L.vsim_model_create.argtypes = [ci, ctypes.POINTER(HParams), ci, ci, ci, ci, ctypes.POINTER(vp)]
     L.vsim_model_load_file.argtypes = [ctypes.c_char_p, ci, ci, ci, ci, ci, ctypes.POINTER(vp)]
     L.vsim_model_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, sz]
+    L.vsim_model_get_tensor.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.vsim_model_randomize.argtypes = [vp, ctypes.c_uint64, cf]
     L.vsim_model_set_mode.argtypes = [vp, ci]
     L.vsim_model_set_graph.argtypes = [vp, ci]
@@ -98,6 +100,8 @@ def lib():
     L.vsim_model_set_profile.argtypes = [vp, ci]
     L.vsim_model_profile_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long),
                                            ctypes.POINTER(ctypes.c_double)]
+    L.vsim_model_profile_kernel.argtypes = [vp, ci, ctypes.c_char_p, ci, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double)]
     L.vsim_dropin_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
     _lib = L
     return L
@@ -157,6 +161,12 @@ class Model:
     def randomize(self, seed=0, std=0.02):
         check(lib().vsim_model_randomize(self.h, seed, std), "randomize")
 
+    def get_tensor(self, name: str, nbytes: int) -> np.ndarray:
+        """One tensor in the ggml file's format (Q4_0 AoS blocks / F32), as raw bytes."""
+        buf = np.zeros(nbytes, np.uint8)
+        check(lib().vsim_model_get_tensor(self.h, name.encode(), ptr(buf), nbytes), f"get_tensor {name}")
+        return buf
+
     def set_mode(self, mode):
         check(lib().vsim_model_set_mode(self.h, mode), "set_mode")
 
@@ -194,6 +204,17 @@ class Model:
         ms, n, b = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         check(lib().vsim_model_profile_stats(self.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "prof")
         return {"gemv_ms": ms.value, "gemv_launches": n.value, "gemv_bytes": b.value}
+
+    def profile_kernels(self) -> list:
+        """Per-kernel totals since set_profile(True): [{name, ms, launches, bytes}]."""
+        out, i = [], 0
+        name = ctypes.create_string_buffer(96)
+        ms, n, b = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
+        while lib().vsim_model_profile_kernel(self.h, i, name, 96, ctypes.byref(ms), ctypes.byref(n),
+                                              ctypes.byref(b)) == 0:
+            out.append({"name": name.value.decode(), "ms": ms.value, "launches": n.value, "bytes": b.value})
+            i += 1
+        return out
 
     def stream(self) -> int:
         return lib().vsim_model_stream(self.h)
