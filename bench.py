@@ -38,13 +38,10 @@ from vsim_amd import pipeline  # noqa: E402
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 GB/s measured copy
 PROMPT = [50278, 12092, 2, 0, 50281]
 ARCHS = {"gptj": hip.ARCH_GPTJ, "gptneox": hip.ARCH_GPTNEOX, "bloom": hip.ARCH_BLOOM}
-# name parts of the Q4_0 GEMV launches (k_layer_tail: fc_out + out-projection, with the
-# attention heads running beside them in the same launch)
-GEMV_KERNELS = ("k_gemv_chain", "k_gemv_solo", "k_layer_tail", "k_gemv_fast")
-# HBM traffic of the GEMV launches, from a separate `rocprofv3 --pmc FETCH_SIZE` pass of this
-# bench (tools/profile_round.sh) committed under profiles/; FETCH_SIZE is in KiB and reads
-# half of the bytes of a 16-byte-per-lane streaming read on gfx950 (MI355X_MICROARCH.md,
-# HBM section), so it is doubled.
+# HBM traffic of the dominant kernel, from a separate `rocprofv3 --pmc FETCH_SIZE` pass of this
+# bench on the same commit (tools/gpu_round.sh) committed under profiles/; FETCH_SIZE is in KiB
+# and reads half of the bytes of a 16-byte-per-lane streaming read on gfx950
+# (MI355X_MICROARCH.md, HBM section), so it is doubled.
 def pmc_file(mode="exact"):
     """The newest profiles/rNN_pmc_fetch_<mode>.csv (tools/gpu_round.sh), or None."""
     import glob
@@ -52,23 +49,61 @@ def pmc_file(mode="exact"):
     return files[-1] if files else None
 
 
-FAST_KERNELS = ("k_fast_gemv", "k_fast_tail", "k_fast_oproj_join")
-
-
-def pmc_traffic_per_launch(path=None, mode="exact"):
-    """Mean corrected FETCH_SIZE bytes per GEMV launch, or None when no PMC pass is committed."""
+def pmc_traffic_per_launch(kernel: str, path=None, mode="exact"):
+    """(mean corrected FETCH_SIZE bytes per launch of `kernel`, source file), or (None, None).
+    Where one kernel serves launches of different shapes (k_gemv_solo: the per-layer batch and
+    the lm_head), the launches of its most frequent grid size are taken: the per-layer one."""
+    import collections
     import csv
     path = path or pmc_file(mode)
     if not path or not os.path.exists(path):
-        return None
-    names = GEMV_KERNELS if mode == "exact" else FAST_KERNELS
-    vals = []
+        return None, None
+    rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            name = r.get("Kernel_Name", "")
-            if r.get("Counter_Name") == "FETCH_SIZE" and any(k in name for k in names):
-                vals.append(float(r["Counter_Value"]) * 1024.0 * 2.0)
-    return sum(vals) / len(vals) if vals else None
+            if r.get("Counter_Name") == "FETCH_SIZE" and kernel in r.get("Kernel_Name", ""):
+                rows.append((r.get("Grid_Size"), float(r["Counter_Value"]) * 1024.0 * 2.0))
+    if not rows:
+        return None, None
+    grid = collections.Counter(g for g, _ in rows).most_common(1)[0][0]
+    vals = [v for g, v in rows if g == grid]
+    return sum(vals) / len(vals), os.path.relpath(path, ROOT)
+
+
+def roofline_from_profile(kernels, wall_s, mode):
+    """The dominant kernel (most device time over the profiled steps): algorithmic bytes per
+    launch / its event-timed average launch, against the HBM peak.  The aggregate over every
+    profiled launch is kept under a separate key."""
+    if not kernels:
+        return None
+    dom = max(kernels, key=lambda k: k["ms"])
+    avg_ms = dom["ms"] / dom["launches"]
+    bpl = dom["bytes"] / dom["launches"]
+    achieved = bpl / (avg_ms * 1e-3) / 1e9
+    rname = dom["name"].split()[0]
+    traffic, src = pmc_traffic_per_launch(rname, mode=mode)
+    tot_ms = sum(k["ms"] for k in kernels)
+    tot_b = sum(k["bytes"] for k in kernels)
+    return {
+        "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+        "frac": round(achieved / PEAK_HBM_GBS, 4),
+        "traffic": round(traffic) if traffic else None,
+        "traffic_source": src,
+        "kernel": dom["name"], "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_ms * 1e3, 3),
+        "launches": dom["launches"],
+        "per_kernel": [{"kernel": k["name"], "launches": k["launches"],
+                        "avg_us": round(1e3 * k["ms"] / k["launches"], 3),
+                        "bytes_per_launch": round(k["bytes"] / k["launches"]),
+                        "GBps": round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1),
+                        "frac": round(k["bytes"] / (k["ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                        "share_of_device_time": round(k["ms"] / tot_ms, 4)} for k in kernels],
+        "aggregate": {"GBps": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
+                      "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                      "device_share_of_wall": round(tot_ms * 1e-3 / wall_s, 4)},
+        "note": ("exact mode is bound by the reference's sequential fp32 add chain per row "
+                 "(K/2 dependent adds), not by HBM: see DESIGN.md 'chain floor'")
+        if mode == "exact" else None,
+    }
 
 
 def metric_name(config: str) -> str:
@@ -84,38 +119,77 @@ def q4_weight_bytes(arch: str, hp: mg.HParams) -> float:
     return 0.625 * (L * (4 * E * E + 2 * E * F) + V * E)
 
 
-def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12):
-    """CPU oracle (port of the reference path) on a bounded sample, tokens/s extrapolated."""
+def host_cpu():
+    """(nproc, lscpu model name, threads available to this process: the box's CPU share)."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:  # the box's CPU share for this job (16 per GPU)
+        avail = min(avail, int(omp))
+    return os.cpu_count() or 1, model, max(1, avail)
+
+
+def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12, n_tokens_1t: int = 4):
+    """CPU oracle (port of the reference path) on a bounded sample, tokens/s extrapolated, at
+    every thread of this job's CPU share and at 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     arch = {"gptneox": 0, "gptj": 1, "bloom": 2}[arch_s]  # VO_ARCH_*
-    nth = max(1, min(16, os.cpu_count() or 1))
-    ctx = 5 + n_tokens + 1
+    nproc, model_name, nth = host_cpu()
 
-    def per_token(n_layer):
-        m = O.Model(None, arch, n_ctx=ctx, synthetic=(hp.n_vocab, hp.n_embd, hp.n_head, n_layer, hp.n_rot, 7, 0.02))
-        m.eval(0, PROMPT, nthreads=nth)
+    def per_token(n_layer, threads, n):
+        m = O.Model(None, arch, n_ctx=5 + n + 1,
+                    synthetic=(hp.n_vocab, hp.n_embd, hp.n_head, n_layer, hp.n_rot, 7, 0.02))
+        m.eval(0, PROMPT, nthreads=threads)
         t0 = time.perf_counter()
-        for i in range(n_tokens):
-            m.eval(5 + i, [i + 11], nthreads=nth)
-        dt = (time.perf_counter() - t0) / n_tokens
+        for i in range(n):
+            m.eval(5 + i, [i + 11], nthreads=threads)
+        dt = (time.perf_counter() - t0) / n
         del m
         return dt
 
-    t1 = per_token(1)
-    t0 = per_token(0)
-    t_layer = max(t1 - t0, 1e-9)
-    t_tok = hp.n_layer * t_layer + t0
+    def tok_time(threads, n):
+        t1 = per_token(1, threads, n)
+        t0 = per_token(0, threads, n)
+        t_layer = max(t1 - t0, 1e-9)
+        return hp.n_layer * t_layer + t0, t_layer, t0
+
+    t_all, tl_all, t0_all = tok_time(nth, n_tokens)
+    t_one, tl_one, t0_one = tok_time(1, n_tokens_1t)
+    speed = None
+    sp = sorted(glob_profiles("*_oracle_vs_ref_speed.json"))
+    if sp:
+        with open(sp[-1]) as f:
+            speed = json.load(f)
     return {
-        "value": round(1.0 / t_tok, 4),
+        "value": round(1.0 / t_all, 4),
         "unit": "tokens/s",
         "cores": nth,
         "kind": "port",
-        "sample": (f"oracle/vsim_oracle.cpp (scalar restatement of imax.c:1182-1230 et al.), {nth} threads; "
-                   f"{n_tokens} decode tokens on a 1-layer and a 0-layer model of {arch_s} width "
-                   f"(E={hp.n_embd}, V={hp.n_vocab}); per-token = {hp.n_layer}*(t1-t0)+t0 = "
-                   f"{t_tok * 1e3:.1f} ms (t_layer {t_layer * 1e3:.1f} ms, t_embed+head {t0 * 1e3:.1f} ms)"),
+        "value_1_thread": round(1.0 / t_one, 4),
+        "host": {"nproc": nproc, "model_name": model_name, "threads_available_to_job": nth},
+        "sample": (f"oracle/vsim_oracle.cpp (scalar restatement of imax.c:1182-1230 et al.); decode tokens "
+                   f"on a 1-layer and a 0-layer model of {arch_s} width (E={hp.n_embd}, V={hp.n_vocab}), "
+                   f"per-token = {hp.n_layer}*(t1-t0)+t0. {nth} threads ({n_tokens} tokens): "
+                   f"{t_all * 1e3:.1f} ms (t_layer {tl_all * 1e3:.1f}, t_embed+head {t0_all * 1e3:.1f}); "
+                   f"1 thread ({n_tokens_1t} tokens): {t_one * 1e3:.1f} ms (t_layer {tl_one * 1e3:.1f}, "
+                   f"t_embed+head {t0_one * 1e3:.1f})"),
+        "oracle_vs_reference_speed": ({"file": os.path.relpath(sp[-1], ROOT), "threads": speed.get("threads")}
+                                      if speed else None),
     }
+
+
+def glob_profiles(pattern):
+    import glob
+    return glob.glob(os.path.join(ROOT, "profiles", pattern))
 
 
 def fast_companion(model, n_past, tok, steps):
@@ -149,8 +223,6 @@ def fast_companion(model, n_past, tok, steps):
     return {"value": round(steps / dt, 3), "unit": "tokens/s", "steps": steps,
             "weight_stream_GBps": round(gbs, 1), "frac_of_peak": round(gbs / PEAK_HBM_GBS, 4),
             "kernels": "k_fast_gemv (LayerNorm prologue), k_fast_tail, k_fast_oproj_join (fast_decode.hip)",
-            "traffic_per_gemv_launch": (round(pmc_traffic_per_launch(mode="fast"))
-                                        if pmc_traffic_per_launch(mode="fast") else None),
             "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": agree / len(rel),
             "parity": "not bit-exact; drifts across steps (tools/mode_drift.py)"}
 
@@ -370,10 +442,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # live roofline of the dominant kernel (Q4_0 GEMV): event pair around every launch,
-    # over a second pass of the same number of decode steps
+    # live roofline of the dominant kernel: an event pair around every launch (per kernel
+    # kind, with its algorithmic bytes), over a second pass of the same decode steps
     roofline = None
-    prof = None
     if not args.no_profile:
         n_past, tok = start
         model.set_profile(True)
@@ -381,24 +452,9 @@ def main():
         run_steps(args.steps)
         torch.cuda.synchronize()
         prof_wall = time.perf_counter() - t1
-        prof = model.profile_stats()
+        kernels = model.profile_kernels()
         model.set_profile(False)
-        if prof["gemv_launches"]:
-            avg_ms = prof["gemv_ms"] / prof["gemv_launches"]
-            bytes_per_launch = prof["gemv_bytes"] / prof["gemv_launches"]
-            achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-            traffic = pmc_traffic_per_launch(mode=args.mode) if args.config == "gpt-j-6B" else None
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 4),
-                        "traffic": round(traffic) if traffic else None,
-                        "kernel": "k_gemv_solo/k_layer_tail/k_gemv_chain32" if args.mode == "exact"
-                        else "k_fast_gemv/k_fast_tail/k_fast_oproj_join",
-                        "bytes_per_launch": round(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 3),
-                        "launches": prof["gemv_launches"],
-                        "gemv_share_of_step": round(prof["gemv_ms"] / 1e3 / prof_wall, 4),
-                        "note": ("exact mode is bound by the reference's sequential fp32 add chain per row "
-                                 "(K/2 dependent adds), not by HBM: see DESIGN.md 'chain floor'")
-                        if args.mode == "exact" else None}
+        roofline = roofline_from_profile(kernels, prof_wall, args.mode)
 
     tokens_total = args.steps * world
     value = tokens_total / elapsed

@@ -120,6 +120,7 @@ struct vsim_model {
     long n = 0;
   };
   bool profile = false;
+  int prof_npast = 0;  // n_past of the step being enqueued (host copy, for the KV byte counts)
   std::vector<hipEvent_t> prof_events;
   std::vector<ProfRec> prof_pending;
   size_t prof_used = 0;
@@ -643,7 +644,7 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
   }
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
   const int nchunk = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
-  const double kv_bytes = 2.0 * ((double)m->npast_host[0] + 1) * E * sizeof(float);
+  const double kv_bytes = 2.0 * ((double)m->prof_npast + 1) * E * sizeof(float);
   float *R[2] = {m->inpL, m->inpL2};
   int cur = 0;
   for (int il = m->l0; il < m->l1; ++il) {
@@ -767,7 +768,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
   // algorithmic bytes of the profiled launches: KV rows read (P + 1) and
   // written by the attention, rows of E floats read / written by the LayerNorm step
-  const double kv_bytes = 2.0 * ((double)m->npast_host[0] + 1) * E * sizeof(float);
+  const double kv_bytes = 2.0 * ((double)m->prof_npast + 1) * E * sizeof(float);
   // reads: the row (+ the four join vectors), each norm's affine; writes: the joined row, each
   // norm's factors xd (E floats) and Q4 row (0.625 B per value)
   auto ln_bytes = [&](int nnorm, bool join) {
@@ -1276,6 +1277,7 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
   if (token < 0 || token >= V) { set_error("eval_argmax: token id out of range"); return VSIM_EINVAL; }
   m->tok_host[0] = token;
   m->npast_host[0] = n_past;
+  m->prof_npast = n_past;
   hipStream_t s = m->stream;
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 1));
@@ -1309,6 +1311,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   hipStream_t s = m->stream;
   m->tok_host[0] = token;
   m->npast_host[0] = n_past;
+  m->prof_npast = n_past;
   RC(upload_step(m));
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 2));
@@ -1316,6 +1319,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   } else {
     for (int i = 0; i < n_steps; ++i) {
       int nk = 0;
+      m->prof_npast = n_past + i;
       RC(enqueue_decode(m, nk));
       RC(launch_argmax_gen(m->logits, m->hp.n_vocab, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s));
     }
@@ -1344,6 +1348,7 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
       VSIM_HIP(hipMemcpyAsync(m->inpL, resid_in, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
     }
     m->npast_host[0] = n_past;
+  m->prof_npast = n_past;
     const bool use_graph = m->graph_enabled && m->first && m->last && !m->profile;
     if (use_graph) {
       // the token / n_past uploads are nodes of the graph (they read the pinned host words
