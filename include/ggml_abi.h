@@ -3,6 +3,9 @@
  *   struct ggml_tensor          ggml.h:275-305
  *   enum ggml_type / ggml_op    ggml.h:217-272
  *   struct ggml_compute_params  ggml.c:1052-1060 (duplicated in imax.c:1115-1121)
+ *   struct ggml_cgraph          ggml.h:308-324
+ *   struct ggml_context         opaque in ggml.h:215; its first two fields (mem_size,
+ *                               mem_buffer, ggml.c:1022-1024) are read by vsim_graph_compute
  * tests/test_capi.py checks offsetof/sizeof of every field against the values the
  * reference objects were compiled with.
  */
@@ -17,6 +20,7 @@
 
 #define VSIM_GGML_MAX_DIMS 4
 #define VSIM_GGML_MAX_OPT 4
+#define VSIM_GGML_MAX_NODES 4096
 
 enum ggml_type {
   GGML_TYPE_Q4_0,
@@ -61,6 +65,25 @@ struct ggml_tensor {
   void *data;
   char padding[8];
 };
+
+struct ggml_cgraph {
+  int n_nodes;
+  int n_leafs;
+  int n_threads;
+
+  size_t work_size;
+  struct ggml_tensor *work;
+
+  struct ggml_tensor *nodes[VSIM_GGML_MAX_NODES];
+  struct ggml_tensor *grads[VSIM_GGML_MAX_NODES];
+  struct ggml_tensor *leafs[VSIM_GGML_MAX_NODES];
+
+  int perf_runs;
+  int64_t perf_cycles;
+  int64_t perf_time_us;
+};
+
+struct ggml_context;
 
 enum ggml_task_type {
   GGML_TASK_INIT = 0,

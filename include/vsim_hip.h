@@ -76,6 +76,28 @@ int vsim_ggml_soft_max_f32(const struct ggml_compute_params *params, const struc
                            struct ggml_tensor *dst);
 int vsim_ggml_mul_mat_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
                           const struct ggml_tensor *src1, struct ggml_tensor *dst);
+/* Device executor for the reference's graph: the drop-in for ggml_graph_compute
+ * (ggml.c:8245-8700, called at vsim.cpp:725 as ggml_graph_compute(ctx0, &gf)).  Walks
+ * cgraph->nodes[] in order on the GPU with the exact-mode kernels; the eval context's arena
+ * (ctx's mem_buffer) and every leaf outside it (model weights, KV cache: mirrored once, then
+ * device-resident) are mirrored at the same offsets, and the last node's bytes are copied
+ * back to its host address.  The KQV product's thread-partial grouping follows
+ * cgraph->n_threads, so the logits equal the reference's at any --threads.
+ * vsim_graph_compute prints the error and exits (as the reference's offload layer does,
+ * imax.c:2042-2049); vsim_graph_compute_rc returns VSIM_E* instead and leaves host memory
+ * untouched when a node is not supported (all nodes are checked before any runs). */
+void vsim_graph_compute(struct ggml_context *ctx, struct ggml_cgraph *cgraph);
+int vsim_graph_compute_rc(struct ggml_context *ctx, struct ggml_cgraph *cgraph);
+/* copy one tensor of the last computed graph back to its host address */
+int vsim_graph_sync_tensor(const struct ggml_tensor *t);
+/* forget every mirror (weights, KV cache, arena) */
+void vsim_graph_reset(void);
+void vsim_graph_stats(uint64_t *computes, uint64_t *nodes, uint64_t *h2d_bytes, uint64_t *d2h_bytes);
+/* per-op device time (event pair per node; also VSIM_GRAPH_PROFILE=1): enable resets the
+ * totals; the report is a text table with the reference's monitor.c row names
+ * (monitor.c:182-262, show_time_sep).  Returns the report's full length. */
+int vsim_graph_set_profile(int enable);
+int vsim_graph_profile_report(char *buf, size_t cap);
 /* drop-in statistics: calls, bytes moved host<->device, device weight-cache size */
 void vsim_dropin_stats(uint64_t *calls, uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *cached_bytes);
 void vsim_dropin_reset(void);

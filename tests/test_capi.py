@@ -84,6 +84,47 @@ def test_ggml_abi_layout():
     assert mine == ref
 
 
+def _cgraph_program(header_include: str) -> str:
+    fields = ["n_nodes", "n_leafs", "n_threads", "work_size", "work", "nodes", "grads", "leafs", "perf_runs",
+              "perf_cycles", "perf_time_us"]
+    lines = [f'printf("{f} %zu\\n", offsetof(struct ggml_cgraph, {f}));' for f in fields]
+    return f"""
+#include <stddef.h>
+#include <stdio.h>
+{header_include}
+int main(void) {{
+  {' '.join(lines)}
+  printf("sizeof %zu\\n", sizeof(struct ggml_cgraph));
+  return 0;
+}}
+"""
+
+
+def test_ggml_cgraph_layout():
+    """vsim_graph_compute reads the reference's struct ggml_cgraph (ggml.h:308-324)."""
+    mine = _run_c(_cgraph_program('#include "ggml_abi.h"'), os.path.join(ROOT, "include"))
+    assert "sizeof" in mine
+    if not os.path.exists(os.path.join(REF, "ggml.h")):
+        pytest.skip("reference headers not present on this machine")
+    ref = _run_c(_cgraph_program('#include <pthread.h>\n#include <signal.h>\n#include "ggml.h"'), REF)
+    assert mine == ref
+
+
+def test_ggml_context_head_layout():
+    """vsim_graph_compute reads mem_size / mem_buffer, the first fields of ggml.c's private
+    struct ggml_context (ggml.c:1022-1024): compile the reference's ggml.c with static
+    assertions on those offsets (compile only, nothing runs)."""
+    if not os.path.exists(os.path.join(REF, "ggml.c")):
+        pytest.skip("reference sources not present on this machine")
+    d = tempfile.mkdtemp()
+    c = os.path.join(d, "t.c")
+    open(c, "w").write(f'#include "{REF}/ggml.c"\n'
+                       "_Static_assert(offsetof(struct ggml_context, mem_size) == 0, \"mem_size\");\n"
+                       "_Static_assert(offsetof(struct ggml_context, mem_buffer) == sizeof(size_t), \"mem_buffer\");\n")
+    subprocess.run(["gcc", "-I", REF, "-pthread", "-fcommon", "-w", "-c", c, "-o", os.path.join(d, "t.o")],
+                   check=True)
+
+
 def test_fp16_tables_match_reference():
     import oracle_py as O
     e_ref, g_ref = O.tables()
