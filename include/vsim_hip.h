@@ -67,7 +67,13 @@ void imax_ggml_compute_forward_mul_mat_q4_0_f32(int THREAD, int LANE, const stru
                                                 const struct ggml_tensor *src0, const struct ggml_tensor *src1,
                                                 struct ggml_tensor *dst);
 /* New hooks (same (params, src0, src1, dst) shape as the static ggml.c kernels they
- * replace; host tensors in, host tensors out, exact mode).  Return 0 if handled. */
+ * replace; host tensors in, host tensors out, exact mode).  Called by every thread of the
+ * reference's pool in every phase: the checks read metadata only, so all threads agree -
+ * either every call returns VSIM_EINVAL (each thread runs its own CPU slice) or thread 0's
+ * COMPUTE call runs the whole op and every call returns 0 (handled; INIT / FINALIZE have
+ * nothing left to do).  mul_mat_f32 takes any strided F32 views; its transposed-src0 branch
+ * (KQV) groups the partial sums by params->nth as ggml.c:4535-4581 + 4469-4493 does.  A
+ * device failure after the checks exits, as the offload layer does (imax.c:2042-2049). */
 int vsim_ggml_gptneox_rope_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
                                const struct ggml_tensor *src1, struct ggml_tensor *dst);
 int vsim_ggml_rope_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,

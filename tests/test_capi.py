@@ -133,3 +133,13 @@ def test_fp16_tables_match_reference():
     hip.check(hip.lib().vsim_op_tables(hip.ptr(e), hip.ptr(g)), "tables")
     assert np.array_equal(e, e_ref)
     assert np.array_equal(g, g_ref)
+
+
+def test_ctypes_ggml_mirror_layout():
+    """vsim_amd.hip.GgmlTensor (the Python callers' mirror) has include/ggml_abi.h's layout."""
+    mine = _run_c(_offsets_program('#include "ggml_abi.h"'), os.path.join(ROOT, "include"))
+    want = dict(ln.split()[:2] for ln in mine.splitlines() if not ln.startswith("GGML_"))
+    import ctypes
+    for name, _ in hip.GgmlTensor._fields_:
+        assert getattr(hip.GgmlTensor, name).offset == int(want[name]), name
+    assert ctypes.sizeof(hip.GgmlTensor) == int(want["sizeof"])

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "graph.hpp"
 #include "../../include/vsim_hip.h"
 
 namespace vsim {
@@ -246,24 +247,89 @@ void vsim_dropin_reset(void) {
 }
 
 // ---- hooks for the reference's static ggml.c kernels (host tensors in/out, exact) ----
+// Contract (include/vsim_hip.h): a hook is called by every thread of the reference's pool in
+// every phase of the node.  Its checks read tensor metadata only, so all threads reach the
+// same verdict: either every thread gets VSIM_EINVAL and runs its own CPU slice, or thread 0
+// runs the whole op in its COMPUTE phase and every other call returns 0 ("handled": the INIT
+// and FINALIZE phases then have nothing left to do).  A device failure after the checks exits,
+// as the reference's offload layer does (imax.c:2042-2049).
+namespace {
+
+size_t f32_span(const ggml_tensor *t) {
+  size_t s = 4;
+  for (int i = 0; i < 4; ++i)
+    if (t->ne[i] > 1) s += (size_t)(t->ne[i] - 1) * t->nb[i];
+  return s;
+}
+
+GT gt_dev(const ggml_tensor *t, const void *dev) {
+  GT g;
+  g.p = (const char *)dev;
+  for (int i = 0; i < 4; ++i) {
+    g.ne[i] = t->ne[i];
+    g.nb[i] = (long long)t->nb[i];
+  }
+  return g;
+}
+
+// cached device buffers of the hooks (grown, never freed per call)
+void *hb[4] = {nullptr, nullptr, nullptr, nullptr};
+size_t hcap[4] = {0, 0, 0, 0};
+double2 *hcs = nullptr;
+size_t hcs_cap = 0;
+
+void *hbuf(int i, size_t bytes, const char *what) {
+  if (grow(&hb[i], &hcap[i], bytes)) die(what);
+  return hb[i];
+}
+
+void to_dev(void *dev, const void *host, size_t bytes) {
+  if (hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, g.stream) != hipSuccess) die("hook upload");
+  g.h2d += bytes;
+}
+
+void to_host(void *host, const void *dev, size_t bytes) {
+  if (hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, g.stream) != hipSuccess ||
+      hipStreamSynchronize(g.stream) != hipSuccess)
+    die("hook download");
+  g.d2h += bytes;
+}
+
+bool handled_elsewhere(const ggml_compute_params *params) {
+  return params->type != GGML_TASK_COMPUTE || params->ith != 0;
+}
+
+void lock_and_init(const char *who) {
+  if (ensure_init()) die(who);
+  if (hipSetDevice(g.device) != hipSuccess) die(who);
+}
+
+}  // namespace
+
 // ggml_compute_forward_gptneox_rope_f32 (ggml.c:6086) / ggml_compute_forward_rope_f32
 // (ggml.c:5919): src0 [d, H, T] contiguous F32, src1 I32 {n_past, n_dims, mode}, in place.
 static int rope_hook(int style, const struct ggml_compute_params *params, const struct ggml_tensor *src0,
                      const struct ggml_tensor *src1, struct ggml_tensor *dst) {
-  if (params->type != GGML_TASK_COMPUTE) return 0;
-  if (params->ith != 0) return 0;
-  std::lock_guard<std::mutex> lk(g.mu);
-  RC(ensure_init());
-  if (!contiguous_f32(src0) || src0->ne[3] != 1 || dst->data != src0->data) {
-    set_error("rope hook: needs a contiguous in-place F32 [d,H,T] tensor");
+  const int32_t *pr = src1 && src1->type == GGML_TYPE_I32 ? (const int32_t *)src1->data : nullptr;
+  if (!contiguous_f32(src0) || src0->ne[3] != 1 || dst->data != src0->data || !pr || pr[1] <= 0 || pr[1] % 2 ||
+      pr[1] > src0->ne[0] || (pr[2] != 0 && pr[2] != 1)) {
+    set_error("rope hook: needs a contiguous in-place F32 [d,H,T] tensor and {n_past, n_dims, mode}");
     return VSIM_EINVAL;
   }
-  const int32_t *pr = (const int32_t *)src1->data;
-  const int d = src0->ne[0], H = src0->ne[1], T = src0->ne[2];
-  RC(upload_tensor(src0, (void **)&g.tmp, &g.tmp_cap));
-  RC(vsim_op_rope(style, g.tmp, d, H, T, pr[0], pr[1], pr[2], g.stream));
-  VSIM_HIP(hipMemcpy(dst->data, g.tmp, (size_t)d * H * T * 4, hipMemcpyDeviceToHost));
-  g.d2h += (size_t)d * H * T * 4;
+  if (handled_elsewhere(params)) return 0;
+  std::lock_guard<std::mutex> lk(g.mu);
+  lock_and_init("rope hook");
+  const int d = src0->ne[0], H = src0->ne[1], T = src0->ne[2], n_past = pr[0], n_dims = pr[1], mode = pr[2];
+  const size_t nb = (size_t)d * H * T * 4;
+  const int n_pos = mode == 0 ? n_past + T : T;
+  std::vector<double2> cs((size_t)n_pos * (n_dims / 2));
+  rope_table_host(cs.data(), n_pos, n_dims);
+  float *x = (float *)hbuf(0, nb, "rope hook alloc");
+  if (grow((void **)&hcs, &hcs_cap, cs.size() * sizeof(double2))) die("rope hook alloc");
+  to_dev(x, src0->data, nb);
+  to_dev(hcs, cs.data(), cs.size() * sizeof(double2));
+  if (launch_rope(style, x, d, H, T, n_past, n_dims, mode, hcs, g.stream)) die("rope hook");
+  to_host(dst->data, x, nb);
   return 0;
 }
 
@@ -281,74 +347,59 @@ int vsim_ggml_rope_f32(const struct ggml_compute_params *params, const struct gg
 // no mask: the reference applies scale and diag_mask_inf as separate nodes before).
 int vsim_ggml_soft_max_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
                            struct ggml_tensor *dst) {
-  if (params->type != GGML_TASK_COMPUTE || params->ith != 0) return 0;
-  std::lock_guard<std::mutex> lk(g.mu);
-  RC(ensure_init());
   if (!contiguous_f32(src0) || dst->data != src0->data) {
     set_error("soft_max hook: needs a contiguous in-place F32 tensor");
     return VSIM_EINVAL;
   }
+  if (handled_elsewhere(params)) return 0;
+  std::lock_guard<std::mutex> lk(g.mu);
+  lock_and_init("soft_max hook");
   const int nc = src0->ne[0], nr = src0->ne[1] * src0->ne[2] * src0->ne[3];
-  RC(upload_tensor(src0, (void **)&g.tmp, &g.tmp_cap));
-  RC(launch_attn_softmax(g.tmp, nc, nr, 1, nc, 1.0f, g.stream));
-  VSIM_HIP(hipMemcpy(dst->data, g.tmp, (size_t)nc * nr * 4, hipMemcpyDeviceToHost));
-  g.d2h += (size_t)nc * nr * 4;
+  const size_t nb = (size_t)nc * nr * 4;
+  float *x = (float *)hbuf(0, nb, "soft_max hook alloc");
+  to_dev(x, src0->data, nb);
+  if (launch_attn_softmax(x, nc, nr, 1, nc, 1.0f, g.stream)) die("soft_max hook");
+  to_host(dst->data, x, nb);
   return 0;
 }
 
-// ggml_compute_forward_mul_mat_f32 (ggml.c:4355): the two attention products of
-// vsim.cpp:583 (K permuted view x Q) and vsim.cpp:607 (V_trans view x softmax).
+// ggml_compute_forward_mul_mat_f32 (ggml.c:4355-4595) for any strided F32 views: src0 rows
+// contiguous -> double-accumulated dots (the KQ product, vsim.cpp:583); src0 transposed ->
+// sequential mads in params->nth column partials, summed in thread order (the KQV product,
+// vsim.cpp:607), the grouping the reference's pool uses at that thread count.
 int vsim_ggml_mul_mat_f32(const struct ggml_compute_params *params, const struct ggml_tensor *src0,
                           const struct ggml_tensor *src1, struct ggml_tensor *dst) {
-  if (params->type != GGML_TASK_COMPUTE || params->ith != 0) return 0;
-  std::lock_guard<std::mutex> lk(g.mu);
-  RC(ensure_init());
-  hipStream_t s = g.stream;
-  const int H = src0->ne[2];
-  if (src0->nb[1] >= src0->nb[0]) {
-    // KQ: src0 [d, nk, H] nb {4, ldk*4, d*4}; src1 [d, N, H] nb {4, ldq*4, d*4}
-    const int d = src0->ne[0], nk = src0->ne[1], N = src1->ne[1];
-    const int ldk = (int)(src0->nb[1] / 4), ldq = (int)(src1->nb[1] / 4);
-    if (src0->nb[0] != 4 || src0->nb[2] != (size_t)d * 4 || src1->nb[0] != 4 || src1->nb[2] != (size_t)d * 4) {
-      set_error("mul_mat_f32 hook: unsupported KQ view");
-      return VSIM_EINVAL;
-    }
-    const size_t kb = ((size_t)(nk - 1) * ldk + (size_t)H * d) * 4, qb = ((size_t)(N - 1) * ldq + (size_t)H * d) * 4;
-    float *dk = nullptr, *dq = nullptr, *dy = nullptr;
-    VSIM_HIP(hipMalloc(&dk, kb));
-    VSIM_HIP(hipMalloc(&dq, qb));
-    VSIM_HIP(hipMalloc(&dy, (size_t)H * N * nk * 4));
-    (void)hipMemcpyAsync(dk, src0->data, kb, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyAsync(dq, src1->data, qb, hipMemcpyHostToDevice, s);
-    int rc = launch_kq(dk, ldk, dq, ldq, d, H, nk, N, dy, s);
-    (void)hipMemcpyAsync(dst->data, dy, (size_t)H * N * nk * 4, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    (void)hipFree(dk); (void)hipFree(dq); (void)hipFree(dy);
-    g.h2d += kb + qb;
-    g.d2h += (size_t)H * N * nk * 4;
-    return rc;
-  }
-  // KQV: src0 = V_trans [nk, d, H] nb {ldv*4, 4, d*4}; src1 = S [nk, N, H] contiguous
-  const int nk = src0->ne[0], d = src0->ne[1], N = src1->ne[1];
-  const int ldv = (int)(src0->nb[0] / 4);
-  if (src0->nb[1] != 4 || src0->nb[2] != (size_t)d * 4 || !contiguous_f32(src1)) {
-    set_error("mul_mat_f32 hook: unsupported KQV view");
+  const bool types = src0->type == GGML_TYPE_F32 && src1->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_F32;
+  const bool shapes = src0->ne[0] == src1->ne[0] && src0->ne[2] == src1->ne[2] && src0->ne[3] == src1->ne[3] &&
+                      dst->ne[0] == src0->ne[1] && dst->ne[1] == src1->ne[1] && dst->ne[2] == src0->ne[2] &&
+                      dst->ne[3] == src1->ne[3];
+  const bool dot = src0->nb[1] >= src0->nb[0];
+  const bool layout = dot ? (src0->nb[0] == 4 && src1->nb[0] == 4 && dst->nb[0] == 4)
+                          : (src0->nb[1] == 4 && contiguous_f32(dst));
+  if (!types || !shapes || !layout || params->nth <= 0) {
+    set_error("mul_mat_f32 hook: unsupported F32 operands");
     return VSIM_EINVAL;
   }
-  const size_t vb = ((size_t)(nk - 1) * ldv + (size_t)H * d) * 4, sb = (size_t)nk * N * H * 4;
-  float *dv = nullptr, *ds = nullptr, *dy = nullptr;
-  VSIM_HIP(hipMalloc(&dv, vb));
-  VSIM_HIP(hipMalloc(&ds, sb));
-  VSIM_HIP(hipMalloc(&dy, (size_t)H * N * d * 4));
-  (void)hipMemcpyAsync(dv, src0->data, vb, hipMemcpyHostToDevice, s);
-  (void)hipMemcpyAsync(ds, src1->data, sb, hipMemcpyHostToDevice, s);
-  int rc = launch_kqv(dv, ldv, ds, d, H, nk, N, dy, 0, s);
-  (void)hipMemcpyAsync(dst->data, dy, (size_t)H * N * d * 4, hipMemcpyDeviceToHost, s);
-  (void)hipStreamSynchronize(s);
-  (void)hipFree(dv); (void)hipFree(ds); (void)hipFree(dy);
-  g.h2d += vb + sb;
-  g.d2h += (size_t)H * N * d * 4;
-  return rc;
+  if (handled_elsewhere(params)) return 0;
+  std::lock_guard<std::mutex> lk(g.mu);
+  lock_and_init("mul_mat_f32 hook");
+  const size_t sa = f32_span(src0), sb = f32_span(src1), sd = f32_span(dst);
+  char *da = (char *)hbuf(1, sa, "mul_mat_f32 hook alloc");
+  char *db = (char *)hbuf(2, sb, "mul_mat_f32 hook alloc");
+  char *dd = (char *)hbuf(3, sd, "mul_mat_f32 hook alloc");
+  to_dev(da, src0->data, sa);
+  to_dev(db, src1->data, sb);
+  int rc;
+  if (dot) {
+    to_dev(dd, dst->data, sd);  // strided dst: the bytes between its elements stay as they were
+    rc = launch_g_mm_dot(gt_dev(dst, dd), gt_dev(src0, da), gt_dev(src1, db), src0->ne[0], g.stream);
+  } else {
+    rc = launch_g_mm_mad((float *)dd, gt_dev(src0, da), gt_dev(src1, db), src1->ne[0], params->nth, dst->ne[0],
+                         dst->ne[1], dst->ne[2], dst->ne[3], g.stream);
+  }
+  if (rc) die("mul_mat_f32 hook");
+  to_host(dst->data, dd, sd);
+  return 0;
 }
 
 }  // extern "C"

@@ -38,6 +38,8 @@ EXPORTS = [
     "vsim_model_stream",
     "vsim_model_logits_dev", "vsim_model_info", "vsim_model_set_graph", "vsim_model_set_profile",
     "vsim_model_profile_kernel", "vsim_model_profile_stats", "vsim_model_free",
+    "vsim_graph_compute", "vsim_graph_compute_rc", "vsim_graph_sync_tensor", "vsim_graph_reset", "vsim_graph_stats",
+    "vsim_graph_set_profile", "vsim_graph_profile_report",
 ]
 
 _lib = None
@@ -45,6 +47,43 @@ _lib = None
 
 class VsimError(RuntimeError):
     pass
+
+
+# ggml ABI mirrors (include/ggml_abi.h; offsets checked against the reference's ggml.h by
+# tests/test_capi.py): for callers that hand host tensors to the drop-in hooks.
+GGML_TYPE_Q4_0, GGML_TYPE_I32, GGML_TYPE_F32 = 0, 4, 6
+GGML_TASK_INIT, GGML_TASK_COMPUTE, GGML_TASK_FINALIZE = 0, 1, 2
+
+
+class GgmlTensor(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("n_dims", ctypes.c_int), ("ne", ctypes.c_int * 4),
+                ("nb", ctypes.c_size_t * 4), ("op", ctypes.c_int), ("is_param", ctypes.c_bool),
+                ("grad", ctypes.c_void_p), ("src0", ctypes.c_void_p), ("src1", ctypes.c_void_p),
+                ("opt", ctypes.c_void_p * 4), ("n_tasks", ctypes.c_int), ("perf_runs", ctypes.c_int),
+                ("perf_cycles", ctypes.c_int64), ("perf_time_us", ctypes.c_int64), ("data", ctypes.c_void_p),
+                ("padding", ctypes.c_char * 8)]
+
+
+class GgmlComputeParams(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("ith", ctypes.c_int), ("nth", ctypes.c_int), ("wsize", ctypes.c_size_t),
+                ("wdata", ctypes.c_void_p)]
+
+
+def ggml_f32(buf, ne, nb=None, typ=GGML_TYPE_F32):
+    """A host ggml_tensor over numpy array `buf` (kept alive by the caller) with shape ne and
+    byte strides nb (contiguous when None)."""
+    ne = list(ne) + [1] * (4 - len(ne))
+    nb = [4] if nb is None else list(nb)
+    while len(nb) < 4:  # the missing outer strides as ggml sets them: nb[i] = nb[i-1] * ne[i-1]
+        nb.append(nb[-1] * ne[len(nb) - 1])
+    t = GgmlTensor()
+    t.type = typ
+    t.n_dims = 4
+    for i in range(4):
+        t.ne[i] = ne[i]
+        t.nb[i] = nb[i]
+    t.data = buf.ctypes.data
+    return t
 
 
 class HParams(ctypes.Structure):
@@ -103,6 +142,15 @@ def lib():
     L.vsim_model_profile_kernel.argtypes = [vp, ci, ctypes.c_char_p, ci, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double)]
     L.vsim_dropin_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+    tp, pp = ctypes.POINTER(GgmlTensor), ctypes.POINTER(GgmlComputeParams)
+    L.vsim_ggml_gptneox_rope_f32.argtypes = [pp, tp, tp, tp]
+    L.vsim_ggml_rope_f32.argtypes = [pp, tp, tp, tp]
+    L.vsim_ggml_soft_max_f32.argtypes = [pp, tp, tp]
+    L.vsim_ggml_mul_mat_f32.argtypes = [pp, tp, tp, tp]
+    L.vsim_graph_compute_rc.argtypes = [vp, vp]
+    L.vsim_graph_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+    L.vsim_graph_set_profile.argtypes = [ci]
+    L.vsim_graph_profile_report.argtypes = [ctypes.c_char_p, sz]
     _lib = L
     return L
 
