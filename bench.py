@@ -248,40 +248,56 @@ def run_pipeline(args, world, rank, dev, dist):
     model.set_graph(not args.no_graph)
     E = hp.n_embd
     host = args.dist_backend == "gloo"
+    first, last = rank == 0, rank == world - 1
     rbuf = torch.empty((len(PROMPT), E), dtype=torch.float32, device="cuda")
     tokt = torch.zeros(1, dtype=torch.int64, device="cpu" if host else "cuda")
+    ext = torch.cuda.ExternalStream(model.stream())
 
     def send(t, dst):
-        dist.send(t.cpu() if host else t, dst=dst)
+        if host:  # gloo: host-staged, after the model's stream has produced the bytes
+            model.sync()
+            dist.send(t.cpu(), dst=dst)
+        else:     # RCCL, ordered on the model's stream (the current stream inside `ext`)
+            dist.send(t, dst=dst)
 
     def recv(t, src):
         if host:
             c = torch.empty(t.shape, dtype=t.dtype)
             dist.recv(c, src=src)
             t.copy_(c)
+            torch.cuda.current_stream().synchronize()
         else:
             dist.recv(t, src=src)
-        torch.cuda.current_stream().synchronize()
 
     def stage(n_past, ids, resid_in, resid_out):
         return model.eval(n_past, ids, resid_in=resid_in, resid_out=resid_out)
 
-    def token_step(n_past, ids):
-        return pipeline.pipeline_step(rank, world, n_past, ids, stage, send, recv, rbuf[:len(ids)], tokt)
-
-    n_past = 0
-    tok = token_step(0, PROMPT)
+    # the prompt: one batched eval through the stages (general path)
+    tok = pipeline.pipeline_step(rank, world, 0, PROMPT, stage, send,
+                                 lambda t, src: (recv(t, src), torch.cuda.current_stream().synchronize()),
+                                 rbuf[:len(PROMPT)], tokt)
     n_past = len(PROMPT)
-    for _ in range(args.warmup):
-        tok = token_step(n_past, [tok])
-        n_past += 1
+    # decode: the device-resident stage step, bound to fixed device buffers
+    tok_dev = torch.tensor([tok if tok is not None else 0], dtype=torch.int32, device="cuda")
+    rin = torch.empty(E, dtype=torch.float32, device="cuda")
+    rout = torch.empty(E, dtype=torch.float32, device="cuda")
+    model.stage_bind(tok_in=tok_dev.data_ptr() if first else 0, resid_in=0 if first else rin.data_ptr(),
+                     resid_out=0 if last else rout.data_ptr(), tok_out=tok_dev.data_ptr() if last else 0)
+    model.stage_begin(n_past)
+    torch.cuda.synchronize()
+
+    def steps(n):
+        with torch.cuda.stream(ext):
+            pipeline.decode_steps(rank, world, model.stage_step, n, send, recv, rin, rout, tok_dev)
+
+    steps(args.warmup)
+    model.sync()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tok = token_step(n_past, [tok])
-        n_past += 1
+    steps(args.steps)
+    model.sync()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -186,6 +186,20 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
  * n_steps generated tokens are copied to tokens_out at the end.  Same tokens as calling
  * vsim_model_eval_argmax n_steps times. */
 int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, int32_t *tokens_out);
+/* Pipeline stage step: the single-token step of this stage's layers between
+ * device buffers the caller binds once -- tok_in (first stage: the token to embed), resid_in
+ * (other stages: the [n_embd] residual from the previous stage), resid_out (non-last stages:
+ * this stage's residual for the next), tok_out (last stage: the greedy token, device argmax,
+ * numpy.argmax conventions).  stage_begin sets n_past on the device; every stage_step
+ * enqueues one step on the model's stream without waiting (captured as a hipGraph when the
+ * graph is on) and advances the device n_past, so a caller can queue steps and the
+ * collective sends / receives between them on that stream without a host round trip.
+ * vsim_model_sync waits for the model's stream. */
+int vsim_model_stage_bind(vsim_model *m, const int32_t *tok_in, const float *resid_in, float *resid_out,
+                          int32_t *tok_out);
+int vsim_model_stage_begin(vsim_model *m, int n_past);
+int vsim_model_stage_step(vsim_model *m);
+int vsim_model_sync(vsim_model *m);
 /* Decode-step timing helpers for bench.py: the stream the executor launches on, and
  * device pointers of the last logits / residual buffers. */
 void *vsim_model_stream(vsim_model *m);

@@ -93,3 +93,60 @@ def test_layer_ranges_tile_the_model():
 @pytest.mark.parametrize("world", [2, 3])
 def test_pipeline_matches_single_rank(world):
     assert _stream(world) == _stream(1)
+
+
+def _run_steps(rank, world, port, out):
+    """pipeline.decode_steps with a stand-in stage step over bound buffers (the device-resident
+    protocol of vsim_model_stage_step: token word in on rank 0, residual rows between ranks,
+    argmax token word out on the last rank), after a pipeline_step prompt."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, last = rank == 0, rank == world - 1
+    l0, l1 = pipeline.layer_range(L, world, rank)
+    kv = {}
+    stage = _stage_fn(l0, l1, first, last, kv)
+    send = (lambda t, dst: dist.send(t, dst=dst)) if world > 1 else None
+    recv = (lambda t, src: dist.recv(t, src=src)) if world > 1 else None
+    prompt = [1, 4, 2]
+    resid = torch.zeros((len(prompt), E), dtype=torch.float32)
+    tok = torch.zeros(1, dtype=torch.int64)
+    first_tok = pipeline.pipeline_step(rank, world, 0, prompt, stage, send, recv, resid, tok)
+    tok[0] = first_tok
+    rin, rout = torch.zeros((1, E)), torch.zeros((1, E))
+    n_past = [len(prompt)]
+    toks = [first_tok]
+
+    def step():
+        logits = stage(n_past[0], [int(tok[0])] if first else None, rin, rout)
+        if last:
+            tok[0] = int(np.argmax(logits))
+        n_past[0] += 1
+
+    pipeline.decode_steps(rank, world, step, 6, send, recv, rin, rout, tok,
+                          record=lambda i: toks.append(int(tok[0])))
+    if last:
+        out.put(toks)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_decode_steps_match_single_rank(world):
+    """The device-resident decode protocol gives the same stream as the per-eval one."""
+    ctx = mp.get_context("spawn")
+
+    def stream(w):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_run_steps, args=(r, w, port, q)) for r in range(w)]
+        for p in procs:
+            p.start()
+        toks = q.get(timeout=120)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        return toks
+
+    assert stream(world) == stream(1) == _stream(1)

@@ -95,6 +95,18 @@ struct vsim_model {
   hipGraphExec_t gexec_gen = nullptr;
   int graph_gen_mode = -1;
   int *hist_dev = nullptr;
+  // pipeline stage step (vsim_model_stage_*): device buffers the caller binds (the token in
+  // on the first stage, the residual in / out between stages, the greedy token out on the
+  // last), a graph of the whole step that ends by advancing n_past on the device, and the
+  // host's count of enqueued steps (n_ctx bound)
+  const int32_t *st_tok_in = nullptr;
+  const float *st_resid_in = nullptr;
+  float *st_resid_out = nullptr;
+  int32_t *st_tok_out = nullptr;
+  hipGraph_t graph_st = nullptr;
+  hipGraphExec_t gexec_st = nullptr;
+  int graph_st_mode = -1;
+  int st_npast = -1;
   unsigned *tail_done = nullptr;  // attention heads finished in the fused layer tail
   // fast-mode decode step (fast_decode.hip): fc_out split-K partial rows and attention
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
@@ -165,6 +177,11 @@ void free_scratch(vsim_model *m) {
   m->graph_gen = nullptr;
   m->graph_gen_mode = -1;
   m->hist_dev = nullptr;
+  if (m->gexec_st) (void)hipGraphExecDestroy(m->gexec_st);
+  if (m->graph_st) (void)hipGraphDestroy(m->graph_st);
+  m->gexec_st = nullptr;
+  m->graph_st = nullptr;
+  m->graph_st_mode = -1;
   if (m->xqa) (void)hipFree(m->xqa);
   if (m->xda) (void)hipFree(m->xda);
   if (m->inpL2) (void)hipFree(m->inpL2);
@@ -1217,15 +1234,41 @@ int upload_step(vsim_model *m) {
   return VSIM_OK;
 }
 
+__global__ void k_npast_advance(int *npast) { npast[0] += 1; }
+
+// One pipeline-stage step from the bound device buffers: token (first stage) or residual
+// (other stages) in, this stage's layers, then the residual out (non-last stages) or the
+// device argmax into the bound token word (last stage), then n_past + 1 on the device.
+int enqueue_stage(vsim_model *m, int &nk) {
+  hipStream_t s = m->stream;
+  const int E = m->hp.n_embd;
+  if (m->first) {
+    VSIM_HIP(hipMemcpyAsync(m->tok_dev, m->st_tok_in, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  } else {
+    VSIM_HIP(hipMemcpyAsync(m->inpL, m->st_resid_in, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  }
+  RC(enqueue_decode(m, nk));
+  if (m->last) {
+    RC(launch_argmax(m->logits, m->hp.n_vocab, m->st_tok_out, s));
+    ++nk;
+  } else {
+    VSIM_HIP(hipMemcpyAsync(m->st_resid_out, m->resid_final, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  }
+  hipLaunchKernelGGL(k_npast_advance, dim3(1), dim3(1), 0, s, m->npast_dev);
+  VSIM_HIP(hipGetLastError());
+  ++nk;
+  return VSIM_OK;
+}
+
 // Capture (once per mode) the whole single-token step as a hipGraph: uploads, the decode
 // kernels, and either the logits copy-out or the device argmax and its 4-byte copy-out.
 // kind 2: the device-resident greedy loop's step -- no uploads, no copy-out; the argmax
 // feeds the next step (launch_argmax_gen).
 int decode_graph(vsim_model *m, int kind) {
-  const bool argmax = kind == 1, gen = kind == 2;
-  hipGraph_t &graph = gen ? m->graph_gen : argmax ? m->graph_am : m->graph;
-  hipGraphExec_t &gexec = gen ? m->gexec_gen : argmax ? m->gexec_am : m->gexec;
-  int &gmode = gen ? m->graph_gen_mode : argmax ? m->graph_am_mode : m->graph_mode;
+  const bool argmax = kind == 1, gen = kind == 2, stage = kind == 3;
+  hipGraph_t &graph = stage ? m->graph_st : gen ? m->graph_gen : argmax ? m->graph_am : m->graph;
+  hipGraphExec_t &gexec = stage ? m->gexec_st : gen ? m->gexec_gen : argmax ? m->gexec_am : m->gexec;
+  int &gmode = stage ? m->graph_st_mode : gen ? m->graph_gen_mode : argmax ? m->graph_am_mode : m->graph_mode;
   if (gexec && gmode == m->mode) return VSIM_OK;
   if (gexec) (void)hipGraphExecDestroy(gexec);
   if (graph) (void)hipGraphDestroy(graph);
@@ -1235,9 +1278,14 @@ int decode_graph(vsim_model *m, int kind) {
   const int V = m->hp.n_vocab;
   VSIM_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
   int gk = 0;
-  int rc = gen ? VSIM_OK : upload_step(m);
-  if (rc == 0) rc = enqueue_decode(m, gk);
-  if (rc == 0 && gen) {
+  int rc = gen || stage ? VSIM_OK : upload_step(m);
+  if (rc == 0 && stage) {
+    rc = enqueue_stage(m, gk);
+  } else if (rc == 0) {
+    rc = enqueue_decode(m, gk);
+  }
+  if (rc == 0 && stage) {
+  } else if (rc == 0 && gen) {
     rc = launch_argmax_gen(m->logits, V, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s);
     ++gk;
   } else if (rc == 0 && argmax) {
@@ -1402,6 +1450,72 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
   if (m->last && logits) memcpy(logits, m->logit_host, sizeof(float) * V);
   m->kernels_last = nk;
   if (m->profile) RC(prof_collect(m));
+  return VSIM_OK;
+}
+
+int vsim_model_stage_bind(vsim_model *m, const int32_t *tok_in, const float *resid_in, float *resid_out,
+                          int32_t *tok_out) {
+  if (!m) { set_error("stage_bind: null model"); return VSIM_EINVAL; }
+  if ((m->first && !tok_in) || (!m->first && !resid_in) || (m->last && !tok_out) || (!m->last && !resid_out)) {
+    set_error("stage_bind: first stage needs tok_in, later stages resid_in, the last tok_out, the others resid_out");
+    return VSIM_EINVAL;
+  }
+  if (!fused_ok(m, 1)) { set_error("stage_bind: needs the single-token decode path"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, 1));
+  if (m->st_tok_in != tok_in || m->st_resid_in != resid_in || m->st_resid_out != resid_out || m->st_tok_out != tok_out) {
+    // the captured step reads the bound addresses: recapture on the next step
+    if (m->gexec_st) (void)hipGraphExecDestroy(m->gexec_st);
+    if (m->graph_st) (void)hipGraphDestroy(m->graph_st);
+    m->gexec_st = nullptr;
+    m->graph_st = nullptr;
+    m->graph_st_mode = -1;
+  }
+  m->st_tok_in = tok_in;
+  m->st_resid_in = resid_in;
+  m->st_resid_out = resid_out;
+  m->st_tok_out = tok_out;
+  return VSIM_OK;
+}
+
+int vsim_model_stage_begin(vsim_model *m, int n_past) {
+  if (!m || n_past < 0 || n_past >= m->n_ctx) { set_error("stage_begin: n_past outside the context"); return VSIM_EINVAL; }
+  if (!m->st_tok_in && !m->st_resid_in) { set_error("stage_begin: stage_bind first"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, 1));
+  m->npast_host[0] = n_past;
+  VSIM_HIP(hipMemcpyAsync(m->npast_dev, m->npast_host, sizeof(int), hipMemcpyHostToDevice, m->stream));
+  VSIM_HIP(hipStreamSynchronize(m->stream));
+  m->st_npast = n_past;
+  return VSIM_OK;
+}
+
+int vsim_model_stage_step(vsim_model *m) {
+  if (!m || m->st_npast < 0) { set_error("stage_step: stage_begin first"); return VSIM_EINVAL; }
+  if (m->st_npast + 1 > m->n_ctx) { set_error("stage_step: context full"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  m->prof_npast = m->st_npast;
+  if (m->graph_enabled && !m->profile) {
+    RC(decode_graph(m, 3));
+    VSIM_HIP(hipGraphLaunch(m->gexec_st, m->stream));
+    m->kernels_last = m->graph_kernels;
+  } else {
+    int nk = 0;
+    RC(enqueue_stage(m, nk));
+    m->kernels_last = nk;
+  }
+  m->st_npast++;
+  if (m->profile) {
+    VSIM_HIP(hipStreamSynchronize(m->stream));
+    RC(prof_collect(m));
+  }
+  return VSIM_OK;
+}
+
+int vsim_model_sync(vsim_model *m) {
+  if (!m) { set_error("sync: null model"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  VSIM_HIP(hipStreamSynchronize(m->stream));
   return VSIM_OK;
 }
 

@@ -40,6 +40,7 @@ EXPORTS = [
     "vsim_model_profile_kernel", "vsim_model_profile_stats", "vsim_model_free",
     "vsim_graph_compute", "vsim_graph_compute_rc", "vsim_graph_sync_tensor", "vsim_graph_reset", "vsim_graph_stats",
     "vsim_graph_set_profile", "vsim_graph_profile_report",
+    "vsim_model_stage_bind", "vsim_model_stage_begin", "vsim_model_stage_step", "vsim_model_sync",
 ]
 
 _lib = None
@@ -148,6 +149,10 @@ def lib():
     L.vsim_ggml_soft_max_f32.argtypes = [pp, tp, tp]
     L.vsim_ggml_mul_mat_f32.argtypes = [pp, tp, tp, tp]
     L.vsim_graph_compute_rc.argtypes = [vp, vp]
+    L.vsim_model_stage_bind.argtypes = [vp, vp, vp, vp, vp]
+    L.vsim_model_stage_begin.argtypes = [vp, ci]
+    L.vsim_model_stage_step.argtypes = [vp]
+    L.vsim_model_sync.argtypes = [vp]
     L.vsim_graph_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
     L.vsim_graph_set_profile.argtypes = [ci]
     L.vsim_graph_profile_report.argtypes = [ctypes.c_char_p, sz]
@@ -266,6 +271,21 @@ class Model:
 
     def stream(self) -> int:
         return lib().vsim_model_stream(self.h)
+
+    def stage_bind(self, tok_in=0, resid_in=0, resid_out=0, tok_out=0):
+        """Bind the pipeline-stage buffers (device addresses, e.g. torch tensors' data_ptr())."""
+        check(lib().vsim_model_stage_bind(self.h, tok_in or None, resid_in or None, resid_out or None,
+                                          tok_out or None), "stage_bind")
+
+    def stage_begin(self, n_past: int):
+        check(lib().vsim_model_stage_begin(self.h, n_past), "stage_begin")
+
+    def stage_step(self):
+        """Enqueue one stage step on the model's stream (no wait)."""
+        check(lib().vsim_model_stage_step(self.h), "stage_step")
+
+    def sync(self):
+        check(lib().vsim_model_sync(self.h), "sync")
 
     def close(self):
         if getattr(self, "h", None):

@@ -10,6 +10,10 @@ the residual row inpL crosses a boundary).  Per eval:
 
 so one residual send per boundary per eval plus the sampled token back to rank 0 (the
 reference's loop feeds the sampled token into the next eval, vsim.cpp:860-891).
+
+pipeline_step runs one eval through host-visible stage calls (the prompt batch);
+decode_steps runs the single-token steps with the device-resident stage step, whose token
+and residual stay in device buffers between the stages.
 """
 from __future__ import annotations
 
@@ -54,3 +58,30 @@ def pipeline_step(rank: int, world: int, n_past: int, ids: Sequence[int],
     if first:
         recv(tok, world - 1)
     return int(tok[0])
+
+
+def decode_steps(rank: int, world: int, step: Callable, n_steps: int, send: Callable, recv: Callable,
+                 resid_in, resid_out, tok, record: Callable | None = None) -> None:
+    """n_steps greedy decode steps through the stages with the device-resident stage step
+    (vsim_model_stage_step): per step and boundary one send of the residual row, and the last
+    stage's device-argmax token back to rank 0, which feeds it to its next step from the same
+    device word.  Nothing crosses to the host, so with a stream-ordered transport (RCCL on the
+    model's stream) the host only queues work.
+
+    step() enqueues this rank's stage step; `tok` is the bound token word (rank 0's tok_in,
+    the last rank's tok_out; one word when world == 1); record(i) runs on the last rank after
+    step i (e.g. to keep the token stream)."""
+    first, last = rank == 0, rank == world - 1
+    for i in range(n_steps):
+        if not first:
+            recv(resid_in, rank - 1)
+        step()
+        if not last:
+            send(resid_out, rank + 1)
+        if last and record is not None:
+            record(i)
+        if world > 1:
+            if last:
+                send(tok, 0)
+            if first:
+                recv(tok, world - 1)
