@@ -200,6 +200,10 @@ int vsim_model_stage_bind(vsim_model *m, const int32_t *tok_in, const float *res
 int vsim_model_stage_begin(vsim_model *m, int n_past);
 int vsim_model_stage_step(vsim_model *m);
 int vsim_model_sync(vsim_model *m);
+/* Test support: size the scratch for n_tokens and fill every scratch buffer and the whole KV
+ * cache with NaN, so that a kernel reading bytes no earlier kernel wrote shows up as a
+ * changed (NaN) result.  Results of later evals must not depend on it. */
+int vsim_model_debug_poison(vsim_model *m, int n_tokens);
 /* Decode-step timing helpers for bench.py: the stream the executor launches on, and
  * device pointers of the last logits / residual buffers. */
 void *vsim_model_stream(vsim_model *m);

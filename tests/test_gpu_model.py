@@ -321,3 +321,34 @@ def test_fast_prefill_deterministic_across_processes(tmp_path):
         outs.append(out)
     for other in outs[1:]:
         subprocess.run([sys.executable, tool, "--compare", outs[0], other], check=True, timeout=120)
+
+
+@pytest.mark.parametrize("arch_name,mode", [("small-gptj", "fast"), ("small-neox", "fast"), ("small-gptj", "exact"),
+                                            ("small-neox", "exact")])
+def test_no_kernel_reads_unwritten_memory(arch_name, mode, tmp_path):
+    """Every scratch buffer and the whole KV cache filled with NaN before the first eval
+    (vsim_model_debug_poison) must not change a single logit bit: no kernel of the prompt path
+    (fast: activation quantize, MFMA GEMM, fp16 K/V copies, MFMA attention; exact: the general
+    path) or of the decode steps reads bytes that no earlier kernel wrote.  Two prompt batches
+    (the second on top of the cache, where fresh memory once changed the bits) and 12 decode
+    steps."""
+    arch_s, hp = mg.CONFIGS[arch_name]
+    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    path = str(tmp_path / "poison.bin")
+    mg.write_model(path, arch_s, hp, seed=6, std=0.05)
+    ids = [(13 * i + 5) % hp.n_vocab for i in range(72)]
+    runs = []
+    for poison in (False, True):
+        m = hip.Model.load(path, arch)
+        m.set_mode(hip.MODE_FAST if mode == "fast" else hip.MODE_EXACT)
+        if poison:
+            m.debug_poison(len(ids))
+        out = [m.eval(0, ids), m.eval(len(ids), ids[:8])]
+        n_past, t = len(ids) + 8, int(np.argmax(out[-1]))
+        for _ in range(12):
+            out.append(m.eval(n_past, [t]))
+            t, n_past = int(np.argmax(out[-1])), n_past + 1
+        runs.append(np.concatenate(out))
+        m.close()
+    assert not np.isnan(runs[1]).any()
+    assert np.array_equal(runs[0].view(np.uint32), runs[1].view(np.uint32))

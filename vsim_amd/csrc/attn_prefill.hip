@@ -273,6 +273,10 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
     return VSIM_EINVAL;
   }
   const int E = d * H, nk = n_past + N;
+  if (E % 64) {  // k_kv_f16 copies 64-column tiles: a partial last tile would be left unwritten
+    set_error("attention prefill: n_embd must be a multiple of 64");
+    return VSIM_EINVAL;
+  }
   const int ldt = (nk + AP_BK - 1) / AP_BK * AP_BK;
   const size_t need = attn_prefill_scratch(E, nk);
   _Float16 *buf = (_Float16 *)scratch;

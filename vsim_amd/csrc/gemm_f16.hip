@@ -225,18 +225,6 @@ int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, fl
   const size_t nbk = (size_t)n * (W.k / QK);
   const uint8_t *xqs = (const uint8_t *)xq;
   const float *xdd = (const float *)(xqs + nbk * 16);
-  // Keep freed stream-ordered memory in the device's pool instead of unmapping it at every
-  // synchronization: the model's prompt layers, which used such per-call operands, gave
-  // second prompt evals that were not bit-stable across processes; with fixed buffers (and
-  // this threshold) they are (tests/test_gpu_model.py).
-  static const bool pool_kept = [] {
-    int dev = 0;
-    hipMemPool_t pool;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return false;
-    uint64_t keep = UINT64_MAX;
-    return hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) == hipSuccess;
-  }();
-  (void)pool_kept;
   _Float16 *x16 = nullptr;
   VSIM_HIP(hipMallocAsync((void **)&x16, nbk * QK * sizeof(_Float16), s));
   hipLaunchKernelGGL(k_act_deq_f16, dim3((unsigned)((nbk + 255) / 256)), dim3(256), 0, s, xqs, xdd, nbk, (half8 *)x16);

@@ -580,7 +580,7 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
-  if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d)) {
+  if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d) && E % 64 == 0) {
     // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
     if (!m->pf_scratch) {  // (prompt evals are never graph-captured: allocating here is safe)
       m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
@@ -1509,6 +1509,34 @@ int vsim_model_stage_step(vsim_model *m) {
     VSIM_HIP(hipStreamSynchronize(m->stream));
     RC(prof_collect(m));
   }
+  return VSIM_OK;
+}
+
+int vsim_model_debug_poison(vsim_model *m, int n_tokens) {
+  if (!m || n_tokens <= 0) { set_error("debug_poison: bad argument"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, n_tokens));
+  const int E = m->hp.n_embd;
+  if (!m->pf_scratch) {
+    m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
+    VSIM_HIP(hipMalloc(&m->pf_scratch, m->pf_bytes));
+  }
+  const size_t n = m->n_max, F = 4 * (size_t)E, V = m->hp.n_vocab, H = m->hp.n_head;
+  const size_t nl = (size_t)std::max(1, m->l1 - m->l0);
+  struct Buf {
+    void *p;
+    size_t bytes;
+  } bufs[] = {
+      {m->inpL, n * E * 4}, {m->cur1, n * E * 4}, {m->cur2, n * E * 4}, {m->Qb, n * E * 4}, {m->Kb, n * E * 4},
+      {m->Vb, n * E * 4}, {m->attn_in, n * E * 4}, {m->attn, n * E * 4}, {m->ff, n * E * 4}, {m->fch, n * F * 4},
+      {m->kq, n * H * m->n_ctx * 4}, {m->logits, V * 4}, {m->xq1, n * E / QK * QBYTES},
+      {m->xq2, n * E / QK * QBYTES}, {m->xq3, n * F / QK * QBYTES}, {m->xd1, n * E * 4}, {m->xd2, n * E * 4},
+      {m->xd3, n * F * 4}, {m->xqa, n * E / QK * QBYTES}, {m->xda, n * E * 4}, {m->inpL2, (size_t)E * 4},
+      {m->pf_scratch, m->pf_bytes & ~(size_t)3}, {m->pf_x16, n >= (size_t)GEMM_MIN_N ? n * (E + F) * 2 : 0},
+      {m->kcache, nl * m->n_ctx * E * 4}, {m->vcache, nl * m->n_ctx * E * 4}};
+  for (const Buf &b : bufs)
+    if (b.p && b.bytes) VSIM_HIP(hipMemsetD32Async((hipDeviceptr_t)b.p, 0x7FC00000u, b.bytes / 4, m->stream));
+  VSIM_HIP(hipStreamSynchronize(m->stream));
   return VSIM_OK;
 }
 

@@ -41,6 +41,7 @@ EXPORTS = [
     "vsim_graph_compute", "vsim_graph_compute_rc", "vsim_graph_sync_tensor", "vsim_graph_reset", "vsim_graph_stats",
     "vsim_graph_set_profile", "vsim_graph_profile_report",
     "vsim_model_stage_bind", "vsim_model_stage_begin", "vsim_model_stage_step", "vsim_model_sync",
+    "vsim_model_debug_poison",
 ]
 
 _lib = None
@@ -153,6 +154,7 @@ def lib():
     L.vsim_model_stage_begin.argtypes = [vp, ci]
     L.vsim_model_stage_step.argtypes = [vp]
     L.vsim_model_sync.argtypes = [vp]
+    L.vsim_model_debug_poison.argtypes = [vp, ci]
     L.vsim_graph_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
     L.vsim_graph_set_profile.argtypes = [ci]
     L.vsim_graph_profile_report.argtypes = [ctypes.c_char_p, sz]
@@ -286,6 +288,10 @@ class Model:
 
     def sync(self):
         check(lib().vsim_model_sync(self.h), "sync")
+
+    def debug_poison(self, n_tokens: int):
+        """Fill the scratch and the KV cache with NaN (test support, include/vsim_hip.h)."""
+        check(lib().vsim_model_debug_poison(self.h, n_tokens), "debug_poison")
 
     def close(self):
         if getattr(self, "h", None):
