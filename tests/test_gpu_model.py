@@ -284,26 +284,6 @@ def test_bloom_cli_greedy_matches_oracle(tmp_path):
     assert tokens(out) == list(want)
 
 
-@pytest.mark.parametrize("cfg", ["small-gptj", "small-neox"])
-def test_layer_kernel_bit_identical(cfg, tmp_path):
-    """The one-launch layer (k_layer_exact, VSIM_LAYER=1 / 2) against the default three-launch
-    layer: same greedy tokens and the same logits bits over 40 decode steps.  The switch is
-    read once per process, so each schedule runs in a child process (tools/layer_ab.py)."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    tool = os.path.join(root, "tools", "layer_ab.py")
-    outs = []
-    for v in ("0", "1", "2"):
-        out = str(tmp_path / f"ab{v}.npz")
-        env = dict(os.environ, VSIM_LAYER=v)
-        subprocess.run([sys.executable, tool, "--config", cfg, "--steps", "40", "--out", out], env=env, check=True,
-                       timeout=300)
-        outs.append(out)
-    for other in outs[1:]:
-        subprocess.run([sys.executable, tool, "--compare", outs[0], other], check=True, timeout=120)
-
-
 def test_fast_prefill_deterministic_across_processes(tmp_path):
     """Two fast prompt evals (96 tokens, then 8 on top of the cache) in separate processes give
     the same logits bits (tools/prefill_ab.py).  In-process repeats reuse every buffer, so

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-shape GEMV timing (GPT-J decode shapes) for the exact and fast kernels.
-usage: python tools/gemv_bench.py [--iters 50]   (env VSIM_GEMV_PC selects the exact variant)"""
+usage: python tools/gemv_bench.py [--iters 50]"""
 import argparse
 import os
 import sys
@@ -72,25 +72,6 @@ def main():
             chain = K / 2 * 7.8 / 2.4e3  # us at 7.8 cycles per dependent add (measured), 2.4 GHz
             print(f"{name:16s} M={M:6d} K={K:6d} {'exact' if mode == 0 else 'fast ':5s} {us:9.2f} us "
                   f"{gbs:8.1f} GB/s  (chain floor {chain:.1f} us)", flush=True)
-            if mode == hip.MODE_EXACT and int(os.environ.get("VSIM_CHAIN_DBG", "0")) & 8:
-                import ctypes
-                buf = (ctypes.c_ulonglong * 64)()
-                L.vsim_debug_chain_prof(buf)
-                nit = max(buf[4], 1)
-                if os.environ.get("VSIM_SOLO"):
-                    print(f"    consumer per iter (ticks): adds {buf[8] / nit:.0f} barrier {buf[9] / nit:.0f}  (iters {nit})")
-                    for w in range(int(os.environ["VSIM_SOLO"])):
-                        b = buf[16 + 4 * w: 19 + 4 * w]
-                        print(f"      producer {w}: top+wait {b[0] / nit:5.0f} compute {b[1] / nit:5.0f} "
-                              f"barrier {b[2] / nit:5.0f}", flush=True)
-                    continue
-                print(f"    producer per iter (cycles): lds-wait {buf[0] / nit:.0f} compute {buf[1] / nit:.0f} "
-                      f"dma+vmwait {buf[2] / nit:.0f} barrier {buf[3] / nit:.0f} | consumer: adds {buf[8] / nit:.0f} "
-                      f"barrier {buf[9] / nit:.0f}  (iters {nit})", flush=True)
-                for w in range(8):
-                    b = buf[16 + 4 * w: 20 + 4 * w]
-                    print(f"      producer {w}: " + " ".join(f"{v / nit:5.0f}" for v in b), flush=True)
-
 
 if __name__ == "__main__":
     main()
