@@ -1126,69 +1126,114 @@ int vsim_model_randomize(vsim_model *m, uint64_t seed, float stddev) {
   return VSIM_OK;
 }
 
+// The ggml model file (vsim.cpp:108-458; convert_gptj_to_ggml.py; convert_bloom_to_ggml.py):
+// header, vocab, then tensor records {n_dims, name_len, ftype, ne[n_dims], name, data} to EOF.
+// Checked as gptneox_model_load checks them (vsim.cpp:398-438): every header field read, every
+// record's name known, its element count and its shape those of the tensor the graph expects
+// (ne[0] = the inner dimension K, ne[1] = rows), its type the expected one, no tensor missing.
+// F32 / F16 weight files (f16 = 0 / 1, vsim.cpp:179-190) take the reference's F32 / F16 mul_mat,
+// which is not this library's path: they are refused with that reason.
 int vsim_model_load_file(const char *path, int arch, int n_ctx, int device, int layer_begin, int layer_end,
                          vsim_model **out) {
+  if (!path || !out) { set_error("load: null argument"); return VSIM_EINVAL; }
   std::ifstream f(path, std::ios::binary);
   if (!f) { set_error(std::string("load: cannot open ") + path); return VSIM_EFILE; }
   auto rd = [&](void *p, size_t n) { f.read((char *)p, n); return (size_t)f.gcount() == n; };
+  auto bad = [](const std::string &why) { set_error("load: " + why); return VSIM_EFILE; };
   uint32_t magic = 0;
-  if (!rd(&magic, 4) || magic != 0x67676d6c) { set_error("load: bad magic"); return VSIM_EFILE; }
+  if (!rd(&magic, 4) || magic != 0x67676d6c) return bad("bad magic");
   vsim_hparams hp{};
   int32_t ftype = 0;
-  rd(&hp.n_vocab, 4); rd(&hp.n_embd, 4);
+  bool ok = rd(&hp.n_vocab, 4) && rd(&hp.n_embd, 4);
   if (arch == VSIM_ARCH_BLOOM) {  // convert_bloom_to_ggml.py:79-85: ..., multiple_of, n_head, n_layer, ftype
     int32_t n_mult = 0;
-    rd(&n_mult, 4);
-    rd(&hp.n_head, 4); rd(&hp.n_layer, 4);
+    ok = ok && rd(&n_mult, 4) && rd(&hp.n_head, 4) && rd(&hp.n_layer, 4);
     hp.n_rot = 0;
   } else {
-    rd(&hp.n_head, 4); rd(&hp.n_layer, 4); rd(&hp.n_rot, 4);
+    ok = ok && rd(&hp.n_head, 4) && rd(&hp.n_layer, 4) && rd(&hp.n_rot, 4);
   }
   hp.use_parallel_residual = arch == VSIM_ARCH_BLOOM ? 0 : 1;
-  if (arch == VSIM_ARCH_GPTNEOX) rd(&hp.use_parallel_residual, 4);
-  rd(&ftype, 4);
-  if (ftype != 2) { set_error("load: only Q4_0 (f16 == 2) files are supported"); return VSIM_EFILE; }
+  if (arch == VSIM_ARCH_GPTNEOX) ok = ok && rd(&hp.use_parallel_residual, 4);
+  ok = ok && rd(&ftype, 4);
+  if (!ok) return bad("truncated header");
+  if (hp.n_vocab <= 0 || hp.n_embd <= 0 || hp.n_head <= 0 || hp.n_layer <= 0 || hp.n_rot < 0)
+    return bad("header values out of range");
+  if (ftype == 0 || ftype == 1)
+    return bad("F32 / F16 weight files take the reference's F32 / F16 mul_mat (vsim.cpp:179-190); this library "
+               "runs the Q4_0 path: quantize the file to Q4_0 (f16 == 2) first");
+  if (ftype != 2) return bad("only Q4_0 (f16 == 2) files are supported");
   int32_t nv = hp.n_vocab;
-  if (arch == VSIM_ARCH_GPTJ) rd(&nv, 4);
+  if (arch == VSIM_ARCH_GPTJ && !rd(&nv, 4)) return bad("truncated vocab count");
+  if (nv < 0 || nv > (1 << 24)) return bad("vocab count out of range");
   for (int i = 0; i < nv; ++i) {
     uint32_t len = 0;
-    if (!rd(&len, 4)) { set_error("load: truncated vocab"); return VSIM_EFILE; }
+    if (!rd(&len, 4) || len > (1u << 20)) return bad("truncated or corrupt vocab");
     f.seekg(len, std::ios::cur);
+    if (!f) return bad("truncated vocab");
   }
   vsim_model *m = nullptr;
   if (layer_end < 0) layer_end = hp.n_layer;
   RC(vsim_model_create(arch, &hp, n_ctx, device, layer_begin, layer_end, &m));
+  std::map<std::string, Slot> full;  // every tensor of the whole model (all stages)
+  {
+    vsim_model whole;
+    whole.arch = arch;
+    whole.hp = hp;
+    whole.l0 = 0;
+    whole.l1 = hp.n_layer;
+    std::vector<std::pair<std::string, Slot>> plan;
+    plan_slots(&whole, plan);
+    for (auto &ps : plan) full[ps.first] = ps.second;
+  }
+  auto fail_load = [&](const std::string &why) {
+    vsim_model_free(m);
+    return bad(why);
+  };
   std::vector<char> buf;
   while (true) {
     int32_t nd = 0, ln = 0, ft = 0;
-    if (!rd(&nd, 4)) break;
-    rd(&ln, 4);
-    rd(&ft, 4);
+    if (!rd(&nd, 4)) break;  // end of file between records
+    if (!rd(&ln, 4) || !rd(&ft, 4)) return fail_load("truncated tensor record");
+    if (nd < 1 || nd > 2 || ln < 1 || ln > 512) return fail_load("corrupt tensor record (n_dims / name length)");
+    int32_t dims[2] = {1, 1};
     size_t ne = 1;
-    int32_t dims[4] = {1, 1, 1, 1};
-    for (int i = 0; i < nd && i < 4; ++i) { rd(&dims[i], 4); ne *= dims[i]; }
+    for (int i = 0; i < nd; ++i) {
+      if (!rd(&dims[i], 4) || dims[i] <= 0) return fail_load("corrupt tensor dimensions");
+      ne *= (size_t)dims[i];
+    }
     std::string name(ln, 0);
-    rd(&name[0], ln);
-    const size_t nbytes = ft == 0 ? ne * 4 : (ft == 2 ? ne / QK * QBYTES : 0);
-    if (nbytes == 0) { vsim_model_free(m); set_error("load: unsupported tensor type in " + name); return VSIM_EFILE; }
-    auto it = m->slots.find(name);
-    if (it == m->slots.end()) it = m->slots.find(name + "/q");  // BLOOM fused qkv
-    if (it == m->slots.end()) {  // tensor of another pipeline stage
+    if (!rd(&name[0], ln)) return fail_load("truncated tensor name");
+    if (ft != 0 && ft != 2) return fail_load("unsupported tensor type in " + name);
+    if (ft == 2 && dims[0] % QK) return fail_load("Q4_0 tensor " + name + " with ne[0] not a multiple of 32");
+    const size_t nbytes = ft == 0 ? ne * 4 : ne / QK * QBYTES;
+    // the tensor as the whole model's graph expects it (BLOOM's fused query_key_value: the
+    // slot of its first row block, three times the rows)
+    const bool fused = full.find(name) == full.end() && full.find(name + "/q") != full.end();
+    auto fit = full.find(fused ? name + "/q" : name);
+    if (fit == full.end()) return fail_load("unknown tensor " + name);
+    const Slot &sl = fit->second;
+    if ((sl.kind == KQ4) != (ft == 2)) return fail_load("type mismatch " + name);
+    const int want_rows = sl.kind == KQ4 ? sl.rows * (fused ? 3 : 1) : 1;
+    if (dims[0] != sl.k || (nd == 2 ? dims[1] : 1) != want_rows) {
+      char msg[256];
+      snprintf(msg, sizeof msg, "tensor %s has the wrong shape in the model file: got [%d, %d], expected [%d, %d]",
+               name.c_str(), dims[0], nd == 2 ? dims[1] : 1, sl.k, want_rows);
+      return fail_load(msg);
+    }
+    if (m->slots.find(fused ? name + "/q" : name) == m->slots.end()) {  // another pipeline stage's tensor
       f.seekg(nbytes, std::ios::cur);
+      if (!f) return fail_load("truncated tensor " + name);
       continue;
     }
     buf.resize(nbytes);
-    if (!rd(buf.data(), nbytes)) { vsim_model_free(m); set_error("load: truncated tensor " + name); return VSIM_EFILE; }
-    if ((it->second.kind == KQ4) != (ft == 2)) { vsim_model_free(m); set_error("load: type mismatch " + name); return VSIM_EFILE; }
-    if (int rc = vsim_model_set_tensor(m, name.c_str(), buf.data(), nbytes)) { vsim_model_free(m); return rc; }
+    if (!rd(buf.data(), nbytes)) return fail_load("truncated tensor " + name);
+    if (int rc = vsim_model_set_tensor(m, name.c_str(), buf.data(), nbytes)) {
+      vsim_model_free(m);
+      return rc;
+    }
   }
   for (auto &kv : m->slots)
-    if (!kv.second.loaded) {
-      std::string n = kv.first;
-      vsim_model_free(m);
-      set_error("load: tensor missing from file: " + n);
-      return VSIM_EFILE;
-    }
+    if (!kv.second.loaded) return fail_load("tensor missing from file: " + kv.first);
   *out = m;
   return VSIM_OK;
 }
