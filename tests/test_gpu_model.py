@@ -22,8 +22,8 @@ CLI = os.path.join(ROOT, "vsim_amd", "_build", "vsim-hip")
 MODELS = sorted(e2e()["models"])
 
 
-def run_cli(args):
-    r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300)
+def run_cli(args, env=None):
+    r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     return r.stdout
 
@@ -332,3 +332,19 @@ def test_no_kernel_reads_unwritten_memory(arch_name, mode, tmp_path):
         m.close()
     assert not np.isnan(runs[1]).any()
     assert np.array_equal(runs[0].view(np.uint32), runs[1].view(np.uint32))
+
+
+def test_cli_per_kernel_time_table(tmp_path):
+    """VSIM_PROFILE=1: vsim-hip ends with a per-kernel device-time table, the counterpart of
+    the reference's per-op table (monitor.c:196-262), and the token stream is unchanged."""
+    arch_s, hp = mg.CONFIGS["small-gptj"]
+    path = str(tmp_path / "prof.bin")
+    mg.write_model(path, arch_s, hp, seed=9, std=0.05)
+    args = ["gptj", "-m", path, "--prompt", "1 2 3 4", "--n_predict", "12", "--top_k", "1", "--seed", "1",
+            "--threads", "1"]
+    plain = run_cli(args)
+    prof = run_cli(args, env=dict(os.environ, VSIM_PROFILE="1"))
+    assert tokens(prof) == tokens(plain)
+    table = prof.split("<END|>", 1)[1]
+    assert "device time per kernel" in table and "COMPUTE (sum)" in table
+    assert "k_layer_tail" in table and "k_gemv_solo" in table or "k_gemv" in table

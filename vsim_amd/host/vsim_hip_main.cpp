@@ -164,6 +164,30 @@ void print_logits(const std::vector<float> &lg, bool end) {
   printf(end ? " <END|>\n" : "\n");
 }
 
+// the per-kernel table of a VSIM_PROFILE=1 run: device ms, share of the device time, launches,
+// average time per launch and algorithmic GB/s (Q4_0 weights at 0.625 B/weight, KV rows)
+void print_kernel_table(vsim_model *model) {
+  struct Row {
+    std::string name;
+    double ms, bytes;
+    long n;
+  };
+  std::vector<Row> rows;
+  char name[128];
+  double ms = 0.0, bytes = 0.0, tot = 0.0;
+  long n = 0;
+  for (int i = 0; vsim_model_profile_kernel(model, i, name, sizeof name, &ms, &n, &bytes) == VSIM_OK; ++i) {
+    rows.push_back({name, ms, bytes, n});
+    tot += ms;
+  }
+  printf("%-54s: %10s %7s %8s %10s %9s\n", "device time per kernel (VSIM_PROFILE=1)", "ms", "share", "launches",
+         "us/launch", "GB/s");
+  for (const Row &r : rows)
+    printf("%-54s: %10.3f %6.1f%% %8ld %10.2f %9.1f\n", r.name.c_str(), r.ms, tot > 0 ? 100.0 * r.ms / tot : 0.0, r.n,
+           r.n ? 1e3 * r.ms / r.n : 0.0, r.ms > 0 ? r.bytes / (r.ms * 1e6) : 0.0);
+  printf("%-54s: %10.3f %6.1f%%\n", "COMPUTE (sum)", tot, 100.0);
+}
+
 int run(const Params &params, int arch) {
   const double t_start = now_s();
   std::mt19937 rng(params.seed);
@@ -175,6 +199,11 @@ int run(const Params &params, int arch) {
   }
   vsim_model_set_mode(model, params.mode);
   vsim_model_set_graph(model, params.graph ? 1 : 0);
+  // VSIM_PROFILE=1: per-kernel device time at the end of the run, the device counterpart of
+  // the reference's per-op time table (monitor.c:196-262, show_time_sep); the steps then run
+  // without their hipGraph, one event pair per launch
+  const bool profile = getenv("VSIM_PROFILE") && atoi(getenv("VSIM_PROFILE")) != 0;
+  if (profile) vsim_model_set_profile(model, 1);
   vsim_hparams hp;
   int n_ctx = 0;
   vsim_model_hparams(model, &hp, &n_ctx, nullptr, nullptr);
@@ -249,6 +278,7 @@ int run(const Params &params, int arch) {
   printf(" <END|>\n");
   printf("\nvsim-hip: load %.3f s, %d evals in %.3f s (%d single-token, %.2f ms/eval), sample %.3f s, total %.3f s\n",
          t_load, n_evals, t_predict, n_decode, n_evals ? 1e3 * t_predict / n_evals : 0.0, t_sample, now_s() - t_start);
+  if (profile) print_kernel_table(model);
   vsim_model_free(model);
   return 0;
 }
