@@ -431,11 +431,7 @@ def main():
         # the next without a host round trip; the same tokens as eval() + numpy.argmax
         # (tests/test_gpu_model.py::test_generate_matches_stepwise_greedy)
         nonlocal n_past, tok
-        if k and arch == hip.ARCH_BLOOM:  # serial residual: general path, host argmax
-            for _ in range(k):
-                tok = int(np.argmax(model.eval(n_past, [tok])))
-                n_past += 1
-        elif k:
+        if k:
             tok = model.generate(n_past, tok, k)[-1]
             n_past += k
 
@@ -498,7 +494,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_fast and args.mode == "exact" and arch != hip.ARCH_BLOOM:
+    if rank == 0 and world == 1 and not args.no_fast and args.mode == "exact":
         # (rewinds to the end of the warm-up: positions are overwritten, n_ctx bounds the rest)
         line["fast_mode"] = fast_companion(model, start[0], start[1], args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -171,28 +171,37 @@ def test_pipeline_stages_equal_single_stage(tmp_path):
         ids = [int(np.argmax(lf))]
 
 
-@pytest.mark.parametrize("cfg", ["small-gptj", "small-neox"])
+@pytest.mark.parametrize("cfg", ["small-gptj", "small-neox", "small-bloom", "small-neox-serial"])
 def test_graph_replay_bit_exact_vs_oracle(cfg, tmp_path):
     """The decode step captured once in a hipGraph and replayed (n_past and the token read
-    from device memory) gives the oracle's logits at every step."""
+    from device memory) gives the oracle's logits at every step; then the device greedy loop
+    (vsim_model_generate) replays the same tokens.  The serial-residual graphs (BLOOM, GPT-NeoX
+    with use_parallel_residual = 0) run their own 6-launch step (model.cpp enqueue_decode)."""
     import oracle_py as O
-    arch_s, hp = mg.CONFIGS[cfg]
-    arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
+    serial = cfg.endswith("-serial")
+    arch_s, hp = mg.CONFIGS[cfg[:-len("-serial")] if serial else cfg]
+    if serial:
+        hp = mg.HParams(hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot, use_parallel_residual=0)
+    arch = {"gptj": hip.ARCH_GPTJ, "gptneox": hip.ARCH_GPTNEOX, "bloom": hip.ARCH_BLOOM}[arch_s]
     path = str(tmp_path / f"{cfg}.bin")
     mg.write_model(path, arch_s, hp, seed=8, std=0.05)
     om = O.Model(path, arch)
     dm = hip.Model.load(path, arch)
+    dm.set_mode(hip.MODE_EXACT)
     dm.set_graph(True)
     ids = [4, 8, 15, 16, 23, 42]
     lo, ld = om.eval(0, ids), dm.eval(0, ids)
     assert np.array_equal(lo.view(np.uint32), ld.view(np.uint32))
-    n_past = len(ids)
+    n_past, toks = len(ids), []
     for step in range(24):
         t = int(np.argmax(lo))
+        toks.append(t)
         lo, ld = om.eval(n_past, [t]), dm.eval(n_past, [t])
         assert np.array_equal(lo.view(np.uint32), ld.view(np.uint32)), step
         n_past += 1
     assert dm.info()["graph"]
+    toks.append(int(np.argmax(lo)))
+    assert dm.generate(len(ids) + 4, toks[4], 20) == toks[5:25]
 
 
 @pytest.mark.parametrize("graph", [True, False])

@@ -120,6 +120,7 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
           }
         }
         sc = sc * A.scale;
+        if (A.alibi) sc = A.alibi[h] + sc;  // (float)(0 + 1) * m_h, added as ggml_alibi does
         if (k < nk) {
           if (l16 == 0) pr[k] = sc;
           mx = mx > sc ? mx : sc;

@@ -101,6 +101,8 @@ struct AttnJob {
   int n_ctx;               // cache rows (sizes the LDS score array, attn_lds_floats)
   int nsplit;              // workgroups per head (column parts of KQV, attn.hpp); 0/1 = one
   float scale;
+  const float *alibi;      // BLOOM: per-head ALiBi slopes (null: none); the single query row
+                           // j = 0 gets (j + 1) * m_h added after the scale (ggml.c:6184-6244)
   uint8_t *oq_qs;          // output activation, Q4 SoA (E/32 blocks)
   float *oq_d, *oxd;
   float *out;              // optional float copy [E]
@@ -113,13 +115,16 @@ __host__ __device__ constexpr int attn_lds_floats(int d, int n_ctx) {
 }
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s);
-// out[i] = x[i] + ((a[i] + ab[i]) + (f[i] + fb[i]))  (ab may be null): the residual join alone
+// out[i] = x[i] + ((a[i] + ab[i]) + (f[i] + fb[i]))  (ab may be null; a null: x[i] + (f[i] + fb[i]),
+// the serial-residual graphs): the residual join alone
 int launch_residual_join(const float *x, const float *a, const float *ab, const float *f, const float *fb, float *out,
                          int n, hipStream_t s);
 int launch_gemv_epi(const GemvBatch &B, int mode, hipStream_t s);
 int launch_attn_decode(const AttnJob &A, int n_ctx, hipStream_t s);
 // exact-mode chain GEMV (gemv_chain.hip): a batch of jobs with the GemvBatch epilogues
 int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s);
+// true when launch_gemv_chain_batch runs B as k_gemv_solo (else k_gemv_chain32)
+bool gemv_chain_solo(const GemvBatch &B);
 
 // ---------------------------------------------------------------- fp16 (ggml.c:95-142)
 __device__ __forceinline__ float bits_f(uint32_t w) { return __uint_as_float(w); }

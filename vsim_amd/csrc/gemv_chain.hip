@@ -482,6 +482,8 @@ static int solo_groups(const GemvBatch &B) {
 // fc_out and the out-projection, whose K = 4E chains are the whole cost).
 constexpr int SOLO_CB = 6, SOLO_PF = 3, SOLO_MIN_GROUPS = 192;
 
+bool gemv_chain_solo(const GemvBatch &B) { return solo_groups(B) >= SOLO_MIN_GROUPS; }
+
 int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
   int tiles = 0;
   for (int i = 0; i < B.nj; ++i) {
@@ -494,7 +496,7 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
   }
   if (tiles == 0) return VSIM_OK;
   const int groups = solo_groups(B);
-  if (groups >= SOLO_MIN_GROUPS) {
+  if (gemv_chain_solo(B)) {
     hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF>), dim3(groups), dim3(64 * SoloShape<SOLO_CB>::WAVES), 0, s, B);
   } else {
     hipLaunchKernelGGL(k_gemv_chain32, dim3(tiles), dim3(C2_THREADS), 0, s, B);

@@ -151,7 +151,9 @@ namespace vsim {
 //    (the map S -> (float)(1/sqrt(S/n+eps)) is monotone) the scale is the reference's.
 // Optional affine y = w*y + b (ggml_add(ggml_mul(repeat(w), cur), repeat(b))).
 // Optional residual join first (the previous layer's, vsim.cpp:694-695): the normalized row is
-// v = x + ((ja + jab) + (jf + jfb)) (jab may be null), written to jout when jout != null.
+// v = x + ((ja + jab) + (jf + jfb)) (jab, jfb may be null), or with one side only (serial
+// residual graphs, vsim.cpp:628, 659 and BLOOM): v = x + (ja + jab) or v = x + (jf + jfb);
+// written to jout when jout != null.
 // stats (optional): [0] mean fallbacks, [1] variance fallbacks.
 // n % 4 == 0; float4 accesses, NT threads x 4 elements per pass, so for n <= 4*NT every load
 // of a pass issues at once (a loop of scalar loads behind branches serialized on their
@@ -182,10 +184,11 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     b0 = ((const float4 *)gb)[i0];
   }
   auto join = [&](int i, float4 v, float4 a, float4 ab, float4 f, float4 fb) {
-    if (ja) {
+    if (ja || jf) {
       if (jab) a = make_float4(a.x + ab.x, a.y + ab.y, a.z + ab.z, a.w + ab.w);
-      v = make_float4(v.x + (a.x + (f.x + fb.x)), v.y + (a.y + (f.y + fb.y)), v.z + (a.z + (f.z + fb.z)),
-                      v.w + (a.w + (f.w + fb.w)));
+      if (jfb) f = make_float4(f.x + fb.x, f.y + fb.y, f.z + fb.z, f.w + fb.w);
+      const float4 t = !jf ? a : !ja ? f : make_float4(a.x + f.x, a.y + f.y, a.z + f.z, a.w + f.w);
+      v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
       if (jout && i >= s0 && i < s1) ((float4 *)jout)[i] = v;
     }
     ((float4 *)row)[i] = v;

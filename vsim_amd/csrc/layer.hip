@@ -62,8 +62,13 @@ __global__ void k_residual_join(const float *x, const float *a, const float *ab,
                                 float *out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const float ff = f[i] + fb[i];
+  if (!a) {  // serial residual: x + (ff + b)
+    out[i] = x[i] + ff;
+    return;
+  }
   const float attn = ab ? a[i] + ab[i] : a[i];
-  out[i] = x[i] + (attn + (f[i] + fb[i]));
+  out[i] = x[i] + (attn + ff);
 }
 
 int launch_residual_join(const float *x, const float *a, const float *ab, const float *f, const float *fb, float *out,

@@ -123,7 +123,7 @@ struct vsim_model {
   // algorithmic bytes it moves (Q4_0 weights at 0.625 B/weight, KV rows, activations).
   struct ProfRec {
     size_t ev;
-    const char *kind;
+    std::string kind;
     double bytes;
   };
   struct ProfKind {
@@ -450,7 +450,7 @@ long prof_begin(vsim_model *m) {
   (void)hipEventRecord(m->prof_events[i], m->stream);
   return (long)i;
 }
-void prof_end(vsim_model *m, long ev, const char *kind, double bytes) {
+void prof_end(vsim_model *m, long ev, const std::string &kind, double bytes) {
   if (ev < 0) return;
   (void)hipEventRecord(m->prof_events[ev + 1], m->stream);
   m->prof_pending.push_back({(size_t)ev, kind, bytes});
@@ -642,6 +642,7 @@ bool fast_decode_ok(const vsim_model *m) {
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H;
   const int nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
   return d % 32 == 0 && d <= 256 && E <= 8192 && E % 128 == 0 &&
+         (m->arch == VSIM_ARCH_GPTJ || (m->arch == VSIM_ARCH_GPTNEOX && m->hp.use_parallel_residual == 1)) &&
          (m->arch == VSIM_ARCH_GPTJ || m->hp.n_rot <= 32) && 2 * H * nch <= 4096;
 }
 
@@ -767,10 +768,19 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
 //      (they join in the next layer's step 1)
 // fc_out's K = 4E chain (vsim.cpp:680-690) is the layer's longest dependency, so the
 // attention branch fills the CUs beside it instead of running before it.
+// Serial-residual graphs (BLOOM; GPT-NeoX with use_parallel_residual = 0, vsim.cpp:626-658)
+// feed the MLP from the attention's residual, so nothing runs beside fc_out; 6 launches:
+//   1. k_ln_quant (join of the previous layer's MLP output +) input LayerNorm
+//   2. GEMV {Q, K, V} (+ bias)
+//   3. k_layer_tail without fc_out: the heads (BLOOM: ALiBi) and the out-projection
+//   4. k_ln_quant: attn + bias + x joined, post-attention LayerNorm (BLOOM keeps the joined
+//      row as the residual, inpFF; GPT-NeoX's serial graph adds the MLP to the old one)
+//   5. GEMV fc_in (+ bias, GELU, requantize)       6. GEMV fc_out
 int enqueue_decode(vsim_model *m, int &nk) {
   if (m->mode == VSIM_MODE_FAST && fast_decode_ok(m)) return enqueue_decode_fast(m, nk);
   const int E = m->hp.n_embd, H = m->hp.n_head, d = E / H, F = 4 * E, V = m->hp.n_vocab;
-  const bool gptj = m->arch == VSIM_ARCH_GPTJ;
+  const bool gptj = m->arch == VSIM_ARCH_GPTJ, bloom = m->arch == VSIM_ARCH_BLOOM;
+  const bool serial = bloom || (!gptj && !m->hp.use_parallel_residual);
   hipStream_t s = m->stream;
   DevTables tab;
   RC(tables_get(&tab));
@@ -778,7 +788,11 @@ int enqueue_decode(vsim_model *m, int &nk) {
   uint8_t *q1 = m->xq1, *q2 = m->xq2, *q3 = m->xq3, *qa = m->xqa;
   float *d1 = (float *)(q1 + (size_t)nbE * 16), *d2 = (float *)(q2 + (size_t)nbE * 16);
   float *d3 = (float *)(q3 + (size_t)nbF * 16), *da = (float *)(qa + (size_t)nbE * 16);
-  if (m->first) {
+  if (m->first && bloom) {  // word embeddings + word_embeddings_layernorm
+    RC(launch_get_rows(m->wte, E, V, m->tok_dev, 1, m->cur1, s));
+    RC(launch_norm(m->cur1, m->inpL, E, 1, m->emb_w, m->emb_b, s));
+    nk += 2;
+  } else if (m->first) {
     RC(launch_get_rows(m->wte, E, V, m->tok_dev, 1, m->inpL, s));
     ++nk;
   }
@@ -797,9 +811,9 @@ int enqueue_decode(vsim_model *m, int &nk) {
   float *R[2] = {m->inpL, m->inpL2};
   int cur = 0;
   bool pending = false;
-  const float *pend_ab = nullptr, *pend_fb = nullptr;
+  const float *pend_a = nullptr, *pend_ab = nullptr, *pend_fb = nullptr;
   auto join_into = [&](LnQuantJob &j, bool write) {
-    j.ja = m->attn;
+    j.ja = pend_a;
     j.jab = pend_ab;
     j.jf = m->ff;
     j.jfb = pend_fb;
@@ -818,9 +832,108 @@ int enqueue_decode(vsim_model *m, int &nk) {
   };
   // the attention heads fuse into k_layer_tail while their LDS (scores over n_ctx) fits it
   const bool tail = m->mode == VSIM_MODE_EXACT && (size_t)attn_lds_floats(d, m->n_ctx) * sizeof(float) <= 75264;
+  auto attn_job = [&](size_t loff) {
+    AttnJob A{};
+    A.q = m->Qb;
+    A.k = m->Kb;
+    A.v = m->Vb;
+    A.kc = m->kcache + loff;
+    A.vc = m->vcache + loff;
+    A.npast = m->npast_dev;
+    A.cs = m->rope_cs;
+    A.etab = tab.exp_f16;
+    A.d = d;
+    A.H = H;
+    A.n_rot = bloom ? 0 : m->hp.n_rot;
+    A.style = gptj ? 1 : 0;
+    A.n_ctx = m->n_ctx;
+    A.nsplit = 1;
+    A.scale = scale;
+    A.alibi = bloom ? m->alibi : nullptr;
+    A.oq_qs = qa;
+    A.oq_d = da;
+    A.oxd = m->xda;
+    A.out = nullptr;
+    return A;
+  };
+  auto gemv = [&](const GemvBatch &Bt, const char *what, double bytes) -> int {
+    const long ev = prof_begin(m);
+    RC(launch_gemv_epi(Bt, m->mode, s));
+    if (ev >= 0)
+      prof_end(m, ev, std::string(m->mode != VSIM_MODE_EXACT ? "k_gemv_fast_epi" : gemv_chain_solo(Bt) ? "k_gemv_solo"
+                                                                                                  : "k_gemv_chain32") +
+                          " (" + what + ")", bytes);
+    ++nk;
+    return VSIM_OK;
+  };
   for (int il = m->l0; il < m->l1; ++il) {
     const LayerW &L = m->layers[il - m->l0];
     const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
+    if (serial) {
+      // 1. (join +) input LayerNorm + quantize
+      LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
+      if (pending) join_into(j1, true);
+      if (tail) j1.clear = m->tail_done;
+      long ev = prof_begin(m);
+      RC(launch_ln_quant(j1, nullptr, E, s));
+      prof_end(m, ev, "k_ln_quant", ln_bytes(1, pending));
+      ++nk;
+      if (pending) cur ^= 1;
+      // 2. Q, K, V (+ bias; BLOOM: the fused query_key_value's row blocks)
+      GemvBatch B{};
+      B.nj = 3;
+      job(B, 0, L.wq, E, E, m->xd1, q1, d1, L.bq, m->Qb);
+      job(B, 1, L.wk, E, E, m->xd1, q1, d1, L.bk, m->Kb);
+      job(B, 2, L.wv, E, E, m->xd1, q1, d1, L.bv, m->Vb);
+      RC(gemv(B, "Q, K, V", 3 * w4_algo_bytes(B.j[0].w)));
+      // 3. heads + out-projection (its bias joins in step 4)
+      const AttnJob A = attn_job(loff);
+      GemvBatch Bo{};
+      Bo.nj = 1;
+      job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
+      if (tail) {
+        GemvBatch none{};
+        ev = prof_begin(m);
+        RC(launch_layer_tail(none, Bo, A, m->tail_done, m->n_ctx, s));
+        prof_end(m, ev, "k_layer_tail (attention + out-proj)", w4_algo_bytes(Bo.j[0].w) + kv_bytes);
+        ++nk;
+      } else {
+        ev = prof_begin(m);
+        RC(launch_attn_decode(A, m->n_ctx, s));
+        prof_end(m, ev, "k_attn_decode", kv_bytes);
+        ++nk;
+        RC(gemv(Bo, "out-proj", w4_algo_bytes(Bo.j[0].w)));
+      }
+      // 4. inpFF = (attn + b_o) + x, post-attention LayerNorm + quantize
+      LnQuantJob j2{R[cur], L.ln2_w, L.ln2_b, q2, d2, m->xd2};
+      j2.ja = m->attn;
+      j2.jab = L.bo;
+      j2.jout = bloom ? R[cur ^ 1] : nullptr;
+      ev = prof_begin(m);
+      RC(launch_ln_quant(j2, nullptr, E, s));
+      prof_end(m, ev, "k_ln_quant", ln_bytes(1, true));
+      ++nk;
+      if (bloom) cur ^= 1;
+      // 5. fc_in (+ bias, GELU, requantize)   6. fc_out (its bias joins in the next step 1)
+      GemvBatch Bi{};
+      Bi.nj = 1;
+      job(Bi, 0, L.wfc, F, E, m->xd2, q2, d2, L.bfc, nullptr);
+      Bi.j[0].epi = EPI_GELU_Q;
+      Bi.j[0].gelu_tab = tab.gelu_f16;
+      Bi.j[0].oq_qs = q3;
+      Bi.j[0].oq_d = d3;
+      Bi.j[0].oxd = m->xd3;
+      RC(gemv(Bi, "fc_in", w4_algo_bytes(Bi.j[0].w)));
+      GemvBatch Bf{};
+      Bf.nj = 1;
+      job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
+      RC(gemv(Bf, "fc_out", w4_algo_bytes(Bf.j[0].w)));
+      pending = true;
+      pend_a = nullptr;
+      pend_ab = nullptr;
+      pend_fb = L.bproj;
+      continue;
+    }
     // 1. (join +) LayerNorm(s) + quantize
     LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
     LnQuantJob j2{R[cur], L.ln2_w, L.ln2_b, q2, d2, m->xd2};
@@ -852,26 +965,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
              w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
     ++nk;
     // 3. attention for the new token (attn.hpp), fc_out and the out-projection
-    AttnJob A{};
-    A.q = m->Qb;
-    A.k = m->Kb;
-    A.v = m->Vb;
-    A.kc = m->kcache + loff;
-    A.vc = m->vcache + loff;
-    A.npast = m->npast_dev;
-    A.cs = m->rope_cs;
-    A.etab = tab.exp_f16;
-    A.d = d;
-    A.H = H;
-    A.n_rot = m->hp.n_rot;
-    A.style = gptj ? 1 : 0;
-    A.n_ctx = m->n_ctx;
-    A.nsplit = 1;
-    A.scale = scale;
-    A.oq_qs = qa;
-    A.oq_d = da;
-    A.oxd = m->xda;
-    A.out = nullptr;
+    const AttnJob A = attn_job(loff);
     GemvBatch Bf{}, Bo{};
     Bf.nj = 1;
     job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
@@ -897,6 +991,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       ++nk;
     }
     pending = true;
+    pend_a = m->attn;
     pend_ab = gptj ? nullptr : L.bo;
     pend_fb = L.bproj;
   }
@@ -917,7 +1012,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
              w4_algo_bytes(B.j[0].w));
     ++nk;
   } else if (pending) {
-    RC(launch_residual_join(R[cur], m->attn, pend_ab, m->ff, pend_fb, R[cur ^ 1], E, s));
+    RC(launch_residual_join(R[cur], pend_a, pend_ab, m->ff, pend_fb, R[cur ^ 1], E, s));
     ++nk;
     cur ^= 1;
   }
@@ -925,9 +1020,8 @@ int enqueue_decode(vsim_model *m, int &nk) {
   return VSIM_OK;
 }
 
-bool fused_ok(const vsim_model *m, int N) {
-  return N == 1 && (m->arch == VSIM_ARCH_GPTJ || m->hp.use_parallel_residual == 1);
-}
+// every graph has a single-token step (the serial-residual ones with 6 launches per layer)
+bool fused_ok(const vsim_model *, int N) { return N == 1; }
 
 thread_local std::string t_err;
 
