@@ -222,7 +222,9 @@ def fast_companion(model, n_past, tok, steps):
     gbs = q4_weight_bytes(arch_s, hp) * steps / dt / 1e9
     return {"value": round(steps / dt, 3), "unit": "tokens/s", "steps": steps,
             "weight_stream_GBps": round(gbs, 1), "frac_of_peak": round(gbs / PEAK_HBM_GBS, 4),
-            "kernels": "k_fast_gemv (LayerNorm prologue), k_fast_tail, k_fast_oproj_join (fast_decode.hip)",
+            "kernels": ("k_gemv_fast_epi GEMVs beside the exact attention and LayerNorm kernels (serial-residual step)"
+                        if model.arch == hip.ARCH_BLOOM else
+                        "k_fast_gemv (LayerNorm prologue), k_fast_tail, k_fast_oproj_join (fast_decode.hip)"),
             "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": agree / len(rel),
             "parity": "not bit-exact; drifts across steps (tools/mode_drift.py)"}
 
