@@ -400,4 +400,19 @@ __device__ __forceinline__ void quantize_block_lanes(float v, int lane, uint8_t 
   }
 }
 
+// One LayerNorm job (join, norm, affine) by one NT-thread workgroup, then quantize_row_q4_0 of
+// the normalized blocks [b0, b1) by whole waves, two 32-blocks per wave step (k_ln_quant: a
+// slice per workgroup).  row: n floats of LDS.
+template <int NT>
+__device__ __forceinline__ void ln_quant_job(const LnQuantJob &J, float *row, int n, unsigned *stats, int b0, int b1) {
+  const int lane = threadIdx.x & 63;
+  ln_exact_lds_t<NT>(J.x, row, n, J.w, J.b, stats, J.ja, J.jab, J.jf, J.jfb, J.jout, b0 * QK / 4, b1 * QK / 4);
+  for (int b2 = threadIdx.x >> 6; b0 + 2 * b2 < b1; b2 += NT / 64) {
+    const int b = b0 + 2 * b2 + (lane >> 5);
+    const bool ok = b < b1;
+    const float v = ok ? row[b * QK + (lane & 31)] : 0.0f;
+    quantize_half(v, lane, ok, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
+  }
+}
+
 }  // namespace vsim

@@ -39,16 +39,9 @@ __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuant
   const int part = blockIdx.x % LNQ_SPLIT;
   const LnQuantJob &J = blockIdx.x < LNQ_SPLIT ? j0 : j1;
   if (J.clear && blockIdx.x == 0 && threadIdx.x < 3) J.clear[64 * threadIdx.x] = 0u;
-  const int nb = n / QK, lane = threadIdx.x & 63;
+  const int nb = n / QK;
   const int b0 = part * nb / LNQ_SPLIT, b1 = (part + 1) * nb / LNQ_SPLIT;  // this slice's blocks
-  ln_exact_lds_t<LNQ_THREADS>(J.x, row, n, J.w, J.b, part == 0 ? stats : nullptr, J.ja, J.jab, J.jf, J.jfb, J.jout,
-                              b0 * QK / 4, b1 * QK / 4);
-  for (int b2 = threadIdx.x >> 6; b0 + 2 * b2 < b1; b2 += LNQ_THREADS / 64) {
-    const int b = b0 + 2 * b2 + (lane >> 5);
-    const bool ok = b < b1;
-    const float v = ok ? row[b * QK + (lane & 31)] : 0.0f;
-    quantize_half(v, lane, ok, J.qs + (size_t)b * 16, J.d + b, J.xd + (size_t)b * QK);
-  }
+  ln_quant_job<LNQ_THREADS>(J, row, n, part == 0 ? stats : nullptr, b0, b1);
 }
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {

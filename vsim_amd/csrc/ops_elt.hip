@@ -215,13 +215,34 @@ __global__ void __launch_bounds__(1024) k_argmax(const float *__restrict__ x, in
   __shared__ int si[16];
   float bv = -INFINITY;
   int bi = 0x7FFFFFFF;
-  for (int i = threadIdx.x; i < n; i += 1024) {
-    const float v = x[i];
+  auto take = [&](float v, int i) {
     if (am_better(v, i, bv, bi)) {
       bv = v;
       bi = i;
     }
+  };
+  // float4 loads, AM_U per thread in flight (a loop of one dependent load per step was bound by
+  // the load latency: ~22 us for a 50k vocabulary); am_better is a total order, so the visiting
+  // order does not change the result
+  constexpr int AM_U = 16;
+  const int n4 = ((uintptr_t)x & 15) ? 0 : n / 4;
+  const float4 *x4 = (const float4 *)x;
+  for (int i0 = threadIdx.x; i0 < n4; i0 += 1024 * AM_U) {
+    float4 v[AM_U];
+#pragma unroll
+    for (int u = 0; u < AM_U; ++u) v[u] = x4[min(i0 + 1024 * u, n4 - 1)];
+#pragma unroll
+    for (int u = 0; u < AM_U; ++u) {
+      const int i = i0 + 1024 * u;
+      if (i < n4) {
+        take(v[u].x, 4 * i);
+        take(v[u].y, 4 * i + 1);
+        take(v[u].z, 4 * i + 2);
+        take(v[u].w, 4 * i + 3);
+      }
+    }
   }
+  for (int i = 4 * n4 + threadIdx.x; i < n; i += 1024) take(x[i], i);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float v = __shfl_xor(bv, o, 64);
