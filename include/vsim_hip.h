@@ -123,6 +123,12 @@ int vsim_op_q4_quantize(const float *x, int k, int n, void *xq, float *xd, void 
  * as ggml_add does, vsim.cpp:545-547) */
 int vsim_op_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias,
                     float *y, int mode, void *stream);
+/* Long-prompt GEMM pieces (fast mode, N >= 256 inside the model): the fp16 image [M][K] of a
+ * W4T32 weight (values d*(q-8) rounded to fp16), and Y[n][m] (+bias[m]) = sum_k W16[m][k] *
+ * X16[n][k] on the 256 x 256-tile fp16 MFMA GEMM (K % 64 == 0; X16 [n][K] fp16). */
+int vsim_op_q4_expand_f16(const void *w, int M, int K, void *w16, void *stream);
+int vsim_op_gemm_f16(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                     void *stream);
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream);
 /* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);

@@ -256,6 +256,37 @@ def test_prefill_gemm_f16(M, K, N):
     assert np.all(np.abs(y - ref) <= 2.0 ** -10 * absum + 1e-5 * (np.abs(b) + 1))
 
 
+@pytest.mark.parametrize("M,K,N", [(520, 512, 300), (256, 64, 256), (1000, 128, 600), (3072, 1024, 512),
+                                   (300, 4096, 257)])
+def test_prefill_gemm_f16_256(M, K, N):
+    """Long-prompt GEMM (gemm_f16.hip k_gemm_f16_256 on the fp16 weight image of
+    k_w4_expand_f16): the image holds exactly the fp16 roundings of d*(q-8); the product is
+    within 4*K*2^-24*sum|w16*x16| of the fp64 product of the same fp16 operands.  Ragged M
+    and N (not multiples of the 256 x 256 tile), K = 64 and 128 (one and two K-tiles: the
+    prologue's and loop's clamped stages), K = 4096."""
+    rng = np.random.default_rng(3 * M + K + N)
+    w_aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05))
+    b = rng.standard_normal(M).astype(np.float32)
+    w = repack(w_aos, M, K)
+    W16 = mg.dequantize_q4_0(w_aos, K).astype(np.float16)
+    img = torch.empty(M * K, dtype=torch.float16, device=DEV)
+    hip.check(hip.lib().vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy().view(np.uint16), W16.reshape(-1).view(np.uint16))
+    X16 = (rng.standard_normal((N, K)) * 0.5).astype(np.float16)
+    x16 = torch.from_numpy(X16).to(DEV)
+    y = torch.empty(N * M, dtype=torch.float32, device=DEV)
+    hip.check(hip.lib().vsim_op_gemm_f16(img.data_ptr(), M, K, x16.data_ptr(), N, dev(b).data_ptr(), y.data_ptr(),
+                                         None), "gemm")
+    torch.cuda.synchronize()
+    y = y.cpu().numpy().reshape(N, M)
+    Wd, Xd = W16.astype(np.float64).reshape(M, K), X16.astype(np.float64)
+    ref = Xd @ Wd.T + b
+    tol = 4.0 * K * 2.0 ** -24 * (np.abs(Xd) @ np.abs(Wd).T) + 1e-6 * np.abs(b)
+    bad = np.abs(y - ref) > tol
+    assert not bad.any(), f"{bad.sum()} of {bad.size} outside the bound, first {np.argwhere(bad)[:4].tolist()}"
+
+
 @pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])
 def test_attn_prefill_f16(d, H, N, n_past):
     """Fast-mode prompt attention (attn_prefill.hip) against fp64 causal attention:

@@ -34,7 +34,7 @@ def bits(a):
 def stats(a, b):
     cos = float(np.dot(a, b) / (np.linalg.norm(a) * np.linalg.norm(b)))
     maxrel = float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
-    return cos, maxrel, int(np.argmax(a)) == int(np.argmax(b))
+    return cos, maxrel, int(np.argmax(a)) == int(np.argmax(b)), int(np.argmax(a)) in np.argsort(b)[-5:]
 
 
 def _model_pair(cfg, tmp_path, seed=5):
@@ -63,12 +63,13 @@ def test_exact_prompt_bit_exact_vs_oracle(cfg, N, tmp_path):
 
 
 @pytest.mark.parametrize("cfg", ["small-gptj", "small-neox", "small-bloom"])
-def test_fast_prompt_vs_oracle(cfg, tmp_path):
+@pytest.mark.parametrize("N", [72, 288])  # 288: the 256 x 256-tile GEMM on the fp16 weight images
+def test_fast_prompt_vs_oracle(cfg, N, tmp_path):
     arch, hp, path, om = _model_pair(cfg, tmp_path)
     res = []
     for seed in range(4):
         rng = np.random.default_rng(seed)
-        ids = [int(v) for v in rng.integers(0, hp.n_vocab, 72)]
+        ids = [int(v) for v in rng.integers(0, hp.n_vocab, N)]
         dm = hip.Model.load(path, arch)
         dm.set_mode(hip.MODE_FAST)
         lo, lf = om.eval(0, ids, nthreads=NTH), dm.eval(0, ids)
@@ -81,7 +82,13 @@ def test_fast_prompt_vs_oracle(cfg, tmp_path):
     msg = f"{cfg}: cos {['%.5f' % c for c in cos]}, max-rel {['%.3g' % r[1] for r in res]}, top-1 {top1}/4"
     print(msg)
     assert min(cos) >= FAST_COS_MIN, msg
-    assert top1 >= 3, msg
+    # the greedy token: the random parity models' top logits are close, and at N = 288 the
+    # re-quantization flips of fast mode move them past each other on either GEMM (r02 A/B:
+    # top-1 2-4/4 with the 128-tile in-LDS-dequant GEMM as with the 256-tile one), so there the
+    # bound is the oracle's top 5
+    if N <= 72:
+        assert top1 >= 3, msg
+    assert all(r[3] for r in res), msg
 
 
 CODEGEN = dict(n_vocab=51200, n_embd=6144, n_head=24, n_layer=1, n_rot=64, use_parallel_residual=1)
@@ -112,7 +119,7 @@ def test_codegen_width_prefill_n2048():
     le = dm.eval(0, ids)
     dm.set_mode(hip.MODE_FAST)
     lf = dm.eval(0, ids)  # same positions: the cache rows are rewritten
-    cos, maxrel, same = stats(lf, le)
+    cos, maxrel, same, _ = stats(lf, le)
     msg = f"codegen-16B width, N=2048: cos {cos:.5f}, max-rel {maxrel:.3g}, top-1 {'same' if same else 'differs'}"
     print(msg)
     assert not np.isnan(lf).any()

@@ -49,6 +49,15 @@ int vsim_op_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd
                     int mode, void *stream) {
   return launch_q4_gemv(w, M, K, xq, xd, n, bias, y, mode, (hipStream_t)stream);
 }
+int vsim_op_q4_expand_f16(const void *w, int M, int K, void *w16, void *stream) {
+  if (!w || !w16 || M <= 0 || K <= 0 || K % QK) { set_error("q4_expand_f16: bad argument"); return VSIM_EINVAL; }
+  return launch_w4_expand_f16(w4_view(w, M, K), w16, (hipStream_t)stream);
+}
+int vsim_op_gemm_f16(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                     void *stream) {
+  if (!w16 || !x16 || !y) { set_error("gemm_f16: null argument"); return VSIM_EINVAL; }
+  return launch_gemm_f16_256(w16, M, K, x16, n, bias, y, (hipStream_t)stream);
+}
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream) {
   return launch_get_rows(w, K, V, rows, n, y, (hipStream_t)stream);
 }

@@ -255,6 +255,15 @@ int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, fl
 constexpr int GEMM_MIN_N = 8;
 int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s);
 int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s);
+// long prompts: fp16 weight images (launch_w4_expand_f16: [M][K], 2 bytes per weight) and the
+// 256 x 256-tile GEMM on them (K % 64 == 0), same operand values as launch_gemm_f16x
+#ifndef VSIM_G2_MIN_N  // (A/B builds: tools/variant.sh with -DVSIM_G2_MIN_N=...)
+#define VSIM_G2_MIN_N 256
+#endif
+constexpr int G2_MIN_N = VSIM_G2_MIN_N;
+int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
+int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                        hipStream_t s);
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call)

@@ -70,22 +70,34 @@ __global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__
 // ggml.c:4113-4152, optional) then quantize_row_q4_0 per 32-block and the dequantized
 // values d*(q-8) as fp16 — what k_q4_quantize + k_act_deq_f16 give, in one pass over the
 // f32 row (which k_gelu would otherwise have read and written once more).  One value per
-// lane, a half-wave per block (q4_half): coalesced 128-byte reads and 64-byte writes.
+// lane, a half-wave per block (q4_half): coalesced 128-byte reads and 64-byte writes; each
+// wave takes AQ_U block pairs with all their loads issued first (one load per lane at a time
+// left the kernel latency-bound at ~1.8 TB/s).
+constexpr int AQ_U = 8;
 __global__ void __launch_bounds__(256) k_act_quant_f16(const float *__restrict__ x, size_t nblk, int nb,
                                                        const float *__restrict__ bias,
                                                        const uint16_t *__restrict__ gelu_tab, _Float16 *__restrict__ X16) {
   const int lane = threadIdx.x & 63;
-  const size_t blk = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-  const bool ok = blk < nblk;  // (uniform per half-wave)
-  const size_t e = blk * QK + (lane & 31);
-  float v = ok ? x[e] : 0.0f;
-  if (gelu_tab && ok) {
-    const float t = bias ? v + bias[(int)(blk % (size_t)nb) * QK + (lane & 31)] : v;
-    v = h2f(gelu_tab[f2h(t)]);
+  const size_t pair0 = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * AQ_U;
+  float v[AQ_U];
+#pragma unroll
+  for (int u = 0; u < AQ_U; ++u) {
+    const size_t blk = (pair0 + u) * 2 + (lane >> 5);
+    v[u] = blk < nblk ? x[blk * QK + (lane & 31)] : 0.0f;
   }
-  float d;
-  const int q = q4_half(v, d);
-  if (ok) X16[e] = (_Float16)(d * (float)(q - 8));
+#pragma unroll
+  for (int u = 0; u < AQ_U; ++u) {
+    const size_t blk = (pair0 + u) * 2 + (lane >> 5);
+    const bool ok = blk < nblk;  // (uniform per half-wave)
+    float t = v[u];
+    if (gelu_tab && ok) {
+      if (bias) t = t + bias[(int)(blk % (size_t)nb) * QK + (lane & 31)];
+      t = h2f(gelu_tab[f2h(t)]);
+    }
+    float d;
+    const int q = q4_half(t, d);
+    if (ok) X16[blk * QK + (lane & 31)] = (_Float16)(d * (float)(q - 8));
+  }
 }
 
 __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16 *__restrict__ X16, int N,
@@ -188,6 +200,201 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16
     }
 }
 
+// ================================================================== fp16 weight image GEMM
+// Long prompts (N >= G2_MIN_N): the Q4_0 weight is expanded once into an fp16 image [M][K]
+// (k_w4_expand_f16: the same halves deq_block_f16 gives), kept by the model per weight, so the
+// GEMM stages both operands by LDS-DMA straight from HBM/L2 and the K loop carries no dequant.
+//
+// k_gemm_f16_256: one 512-thread workgroup per 256 x 256 output tile (8 waves: 2 along M x 4
+// along N, 128 x 64 each, v_mfma_f32_16x16x32_f16, 32 accumulators of 4), K in tiles of 64.
+// LDS: two buffers x {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255} of 16 KB
+// ("half-tiles", [128 rows][64 halves], 16-byte chunks XOR-swizzled by (row >> 1) & 7 so the
+// 16 lanes of a ds_read_b128 group hit 16 different bank slots).  Each K-tile is 4 phases, one
+// output quadrant (64 x 32 per wave, 16 MFMAs) per phase, and one half-tile staged per phase:
+//   P1: read A rows 0-63 + B cols 0-31, stage A h0 of tile t+1
+//   P2: read B cols 32-63,             stage A h1 of tile t+1
+//   P3: read A rows 64-127,            stage B h0 of tile t+2
+//   P4: (B cols 0-31 still held),      stage B h1 of tile t+2; vmcnt(4)
+// A half of buffer b is last read in P3 of its tile, a B half in P2, so each is restaged at
+// least one phase (and a barrier) after its last read; vmcnt(4) at the end of P4 retires
+// everything but the two B half-tiles of t+2, i.e. all of tile t+1, before the barrier that
+// precedes its first read.  The DMA stays in flight across the raw s_barriers (no vmcnt(0) in
+// the loop; cdna_hip_programming.md §5 "256² 8-phase template").  Workgroups are remapped so
+// each XCD takes a contiguous range of tiles (neighbours share A rows in that XCD's L2).
+constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64, G2_THREADS = 512;
+constexpr int G2_HALF = 128 * G2_BK;  // halves per half-tile (16 KB)
+constexpr int G2_LDS = 2 * 4 * G2_HALF * 2;  // bytes: 128 KB
+
+__global__ void __launch_bounds__(256) k_w4_expand_f16(W4 W, half8 *__restrict__ out) {
+  const int nb = W.k / QK;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (row, block), blocks of a row adjacent
+  if (i >= (size_t)W.rows * nb) return;
+  const int row = (int)(i / nb), b = (int)(i % nb);
+  const size_t o = ((size_t)(row / T32) * nb + b) * T32 + (row & (T32 - 1));
+  half8 h[4];
+  deq_block_f16(*(const uint4 *)(W.qs + o * 16), W.d[o], h);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) out[4 * i + w] = h[w];
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
+                                                                 const _Float16 *__restrict__ B, int N,
+                                                                 const float *__restrict__ bias, float *__restrict__ Y) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2, wc = wave & 3;
+  const int tm = (M + G2_BM - 1) / G2_BM, tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
+  // XCD remap (bijective): the blocks dispatched to one XCD (bid % 8) take consecutive tiles
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (wg / tn) * G2_BM, n0 = (wg % tn) * G2_BN;
+  const int nk = K / G2_BK;
+  const uint32_t lbase = lds_addr(g2lds);
+  // stage half-tile `part` (0/1: A rows h*128.., 2/3: B rows) of K-tile kt into buffer kt & 1;
+  // the source tile is clamped to the last one (the loads past the end fill a buffer that is
+  // not read again, and keep the per-wave DMA count of every phase the same)
+  auto stage = [&](int kt, int part) {
+    const int kc = min(kt, nk - 1);
+    const bool isA = part < 2;
+    const int h = part & 1;
+    const _Float16 *src = isA ? A : B;
+    const int lim = (isA ? M : N) - 1, r00 = (isA ? m0 : n0) + h * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rb = (j * 8 + wave) * 8;      // first row (within the half) of this instruction
+      const int r = rb + (lane >> 3);         // this lane's row
+      const int c = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at LDS chunk lane & 7
+      const _Float16 *g = src + (size_t)min(r00 + r, lim) * K + (size_t)kc * G2_BK + 8 * c;
+      glds16<false>(g, lbase + (uint32_t)((((kt & 1) * 4 + part) * G2_HALF + rb * G2_BK) * 2));
+    }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  half8 a[4][2], b0[2][2], b1[2][2];
+  const int fr = lane & 15, fk = lane >> 4;
+  auto rd = [&](const _Float16 *half, int row, int kk) {  // fragment: 8 halves of `row` at k 8*fk + 32*kk
+    const int c = kk * 4 + fk;
+    return *(const half8 *)(half + row * G2_BK + 8 * (c ^ ((row >> 1) & 7)));
+  };
+  auto rdA = [&](int buf, int mh) {
+    const _Float16 *hp = g2lds + (buf * 4 + wr) * G2_HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = rd(hp, (4 * mh + i) * 16 + fr, kk);
+  };
+  auto rdB = [&](half8 (&bb)[2][2], int buf, int nh) {
+    const _Float16 *hp = g2lds + (buf * 4 + 2 + (wc >> 1)) * G2_HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bb[j][kk] = rd(hp, (wc & 1) * 64 + (2 * nh + j) * 16 + fr, kk);
+  };
+  auto mma = [&](int mh, int nh, const half8 (&bb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * mh + i][2 * nh + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][kk], bb[j][kk], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define G2_SYNC_MMA(MH, NH, BB)                        \
+  __builtin_amdgcn_sched_barrier(0);                   \
+  __builtin_amdgcn_s_barrier();                        \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+  mma(MH, NH, BB);                                     \
+  __builtin_amdgcn_sched_barrier(0);
+  // prologue: tile 0 whole, tile 1's B halves in flight
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 0);
+  stage(0, 1);
+  stage(1, 2);
+  stage(1, 3);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const int cb = t & 1;
+    rdA(cb, 0);
+    rdB(b0, cb, 0);
+    stage(t + 1, 0);
+    G2_SYNC_MMA(0, 0, b0)
+    __builtin_amdgcn_s_barrier();
+    rdB(b1, cb, 1);
+    stage(t + 1, 1);
+    G2_SYNC_MMA(0, 1, b1)
+    __builtin_amdgcn_s_barrier();
+    rdA(cb, 1);
+    stage(t + 2, 2);
+    G2_SYNC_MMA(1, 1, b1)
+    __builtin_amdgcn_s_barrier();
+    stage(t + 2, 3);
+    G2_SYNC_MMA(1, 0, b0)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#undef G2_SYNC_MMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
+  // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + 4 * fk;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = m + e < M ? bias[m + e] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + fr;
+      if (n >= N) continue;
+      const float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+      float *dst = Y + (size_t)n * M + m;
+      if ((M & 3) == 0 && m + 3 < M) {
+        *(float4 *)dst = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (m + e < M) dst[e] = v[e];
+      }
+    }
+  }
+}
+
+int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s) {
+  const size_t n = (size_t)W.rows * (W.k / QK);
+  hipLaunchKernelGGL(k_w4_expand_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, (half8 *)out);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                        hipStream_t s) {
+  if (K % G2_BK || K <= 0 || M <= 0 || n <= 0) {
+    set_error("f16 gemm: K must be a positive multiple of 64");
+    return VSIM_EINVAL;
+  }
+  static bool attr = false;
+  if (!attr) {
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));
+    attr = true;
+  }
+  const int nwg = ((M + G2_BM - 1) / G2_BM) * ((n + G2_BN - 1) / G2_BN);
+  hipLaunchKernelGGL(k_gemm_f16_256, dim3(nwg), dim3(G2_THREADS), G2_LDS, s, (const _Float16 *)A16, M, K,
+                     (const _Float16 *)x16, n, bias, y);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
 int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s) {
   if (K % QK || n <= 0) {
     set_error("act_quant_f16: K must be a multiple of 32");
@@ -200,7 +407,8 @@ int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool g
     tab = t.gelu_f16;
   }
   const size_t nblk = (size_t)n * (K / QK);
-  hipLaunchKernelGGL(k_act_quant_f16, dim3((unsigned)((nblk + 7) / 8)), dim3(256), 0, s, x, nblk, K / QK, bias, tab,
+  const size_t per_wg = 4 * 2 * AQ_U;  // blocks per workgroup
+  hipLaunchKernelGGL(k_act_quant_f16, dim3((unsigned)((nblk + per_wg - 1) / per_wg)), dim3(256), 0, s, x, nblk, K / QK, bias, tab,
                      (_Float16 *)x16);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;

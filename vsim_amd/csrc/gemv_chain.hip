@@ -31,8 +31,6 @@ typedef const __attribute__((address_space(4))) float sfloat;  // scalar-loaded
 typedef const __attribute__((address_space(1))) u32x4 gu32x4;  // global, for nontemporal loads
 typedef const __attribute__((address_space(1))) float gfloat;
 
-__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
-
 // Producer-side barrier without the lgkmcnt(0) of __syncthreads: it would also wait for the
 // scalar loads of the next chunk's activation factors still in flight.  The pair terms
 // written before it are first read by the consumer one whole chunk later (it reads chunk
@@ -41,19 +39,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(
 // stores across.
 __device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-// LDS-DMA: each lane's 16 (4) bytes from its own global address land lane-linearly at the
-// wave-uniform LDS address.  Inline asm keeps the load out of the compiler's wait-count
-// bookkeeping: completion is retired by the explicit vmcnt waits.  nt: streamed once.
-__device__ __forceinline__ void glds16(const void *g, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-__device__ __forceinline__ void glds4(const void *g, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
 
 // ================================================================== 32-row variant
 // Same chain and producer/consumer protocol for one W4T32 tile (32 rows) per workgroup, so a

@@ -126,6 +126,28 @@ __device__ __forceinline__ void pair_terms4_x(uint32_t w, f32x2 d512, f32x2 m2, 
   p4[3] = t23.y;
 }
 
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
+
+// LDS-DMA: each lane's 16 (4) bytes from its own global address land lane-linearly at the
+// wave-uniform LDS address.  Inline asm keeps the load out of the compiler's wait-count
+// bookkeeping: completion is retired by the explicit vmcnt waits.  nt: streamed once (the
+// GEMV weights); without it the lines stay in L2 for the other workgroups (GEMM operands).
+template <bool NT = true>
+__device__ __forceinline__ void glds16(const void *g, uint32_t lds) {
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+
 constexpr int NORM_THREADS = 256;
 
 __device__ __forceinline__ int ulp_exp(float x) {

@@ -112,6 +112,10 @@ struct vsim_model {
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
   float *fast_ffp = nullptr, *fast_part = nullptr;
   void *pf_scratch = nullptr;  // fast prefill: fp16 K / V^T copies (attn_prefill.hip)
+  // fast prefill of long prompts: fp16 images [M][K] of the Q4_0 weights (2 bytes per weight,
+  // made on first use, dropped when a weight changes), for the 256 x 256-tile GEMM
+  std::map<const void *, void *> w16;
+  size_t w16_bytes = 0;
   void *pf_x16 = nullptr;      // fast prefill: fp16 GEMM operands, [n_max][E] then [n_max][4E]
   size_t pf_bytes = 0;
 
@@ -142,6 +146,12 @@ struct vsim_model {
 namespace {
 
 int E_(const vsim_model *m) { return m->hp.n_embd; }
+
+void free_w16(vsim_model *m) {
+  for (auto &kv : m->w16) (void)hipFree(kv.second);
+  m->w16.clear();
+  m->w16_bytes = 0;
+}
 
 void free_scratch(vsim_model *m) {
   void *ps[] = {m->inpL, m->cur1, m->cur2, m->Qb, m->Kb, m->Vb, m->attn_in, m->attn, m->ff, m->fch, m->kq,
@@ -484,6 +494,22 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
   if (quantize && !x16) {
     RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
     ++nk;
+  }
+  if (x16 && N >= G2_MIN_N && K % 64 == 0) {
+    // long prompt: the 256 x 256-tile GEMM on the weight's fp16 image
+    void *&img = m->w16[W];
+    if (!img) {
+      const size_t bytes = (size_t)M * K * sizeof(uint16_t);
+      VSIM_HIP(hipMalloc(&img, bytes));
+      m->w16_bytes += bytes;
+      RC(launch_w4_expand_f16(w4_view(W, M, K), img, m->stream));
+      ++nk;
+    }
+    const long ev = prof_begin(m);
+    RC(launch_gemm_f16_256(img, M, K, x16, N, bias, y, m->stream));
+    prof_end(m, ev, "k_gemm_f16_256 (prompt)", (double)M * K / QK * QBYTES);
+    ++nk;
+    return VSIM_OK;
   }
   const long ev = prof_begin(m);
   if (x16) {
@@ -1130,6 +1156,7 @@ void vsim_model_free(vsim_model *m) {
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   if (m->alibi) (void)hipFree(m->alibi);
   free_scratch(m);
+  free_w16(m);
   if (m->warena) (void)hipFree(m->warena);
   if (m->kcache) (void)hipFree(m->kcache);
   if (m->vcache) (void)hipFree(m->vcache);
@@ -1140,6 +1167,10 @@ void vsim_model_free(vsim_model *m) {
 }
 
 int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes) {
+  if (!m->w16.empty()) {  // fp16 weight images are remade from the new weights on next use
+    (void)hipStreamSynchronize(m->stream);
+    free_w16(m);
+  }
   {  // BLOOM's fused query_key_value weight: three [E][E] row blocks, q | k | v
     const std::string n(name), suf = "attention.query_key_value.weight";
     if (m->arch == VSIM_ARCH_BLOOM && n.size() >= suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0) {
@@ -1203,6 +1234,10 @@ int vsim_model_get_tensor(vsim_model *m, const char *name, void *host, size_t nb
 
 int vsim_model_randomize(vsim_model *m, uint64_t seed, float stddev) {
   VSIM_HIP(hipSetDevice(m->device));
+  if (!m->w16.empty()) {
+    VSIM_HIP(hipStreamSynchronize(m->stream));
+    free_w16(m);
+  }
   uint64_t id = 0;
   for (auto &kv : m->slots) {
     Slot &s = kv.second;
