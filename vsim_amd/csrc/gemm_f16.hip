@@ -210,17 +210,21 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16
 // LDS: two buffers x {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255} of 16 KB
 // ("half-tiles", [128 rows][64 halves], 16-byte chunks XOR-swizzled by (row >> 1) & 7 so the
 // 16 lanes of a ds_read_b128 group hit 16 different bank slots).  Each K-tile is 4 phases, one
-// output quadrant (64 x 32 per wave, 16 MFMAs) per phase, and one half-tile staged per phase:
+// output quadrant (64 x 32 per wave, 16 MFMAs) per phase; a phase is {LDS reads, DMA issue}
+// barrier {MFMAs} barrier.  The two wave groups (waves 0-3: A rows 0-127, waves 4-7: rows
+// 128-255; one of each per SIMD) run one barrier apart, so on every SIMD one wave's MFMAs
+// overlap the other's LDS reads (group 1 takes one extra barrier first, group 0 one last):
 //   P1: read A rows 0-63 + B cols 0-31, stage A h0 of tile t+1
 //   P2: read B cols 32-63,             stage A h1 of tile t+1
-//   P3: read A rows 64-127,            stage B h0 of tile t+2
-//   P4: (B cols 0-31 still held),      stage B h1 of tile t+2; vmcnt(4)
-// A half of buffer b is last read in P3 of its tile, a B half in P2, so each is restaged at
-// least one phase (and a barrier) after its last read; vmcnt(4) at the end of P4 retires
-// everything but the two B half-tiles of t+2, i.e. all of tile t+1, before the barrier that
-// precedes its first read.  The DMA stays in flight across the raw s_barriers (no vmcnt(0) in
-// the loop; cdna_hip_programming.md §5 "256² 8-phase template").  Workgroups are remapped so
-// each XCD takes a contiguous range of tiles (neighbours share A rows in that XCD's L2).
+//   P3: read A rows 64-127,            wait for all of tile t+1 (vmcnt(0))
+//   P4: (B cols 0-31 still held),      stage B h0 and B h1 of tile t+2
+// With the groups a barrier apart, a half-tile is restaged >= 2 phases after its last read (A
+// halves: read up to P3, restaged in P1/P2 of the next tile; B halves: read up to P2, restaged
+// in P4) and read >= 2 phases after the wait that retires it (tile t+1 waited in P3 of tile t,
+// first read in P1 of tile t+1) -- cdna_hip_programming.md §5 ("read a staged buffer one
+// phase after the wait", "one barrier more when two wave groups run staggered").  The DMA
+// stays in flight across the raw s_barriers.  Workgroups are remapped so each XCD takes a
+// contiguous range of tiles (neighbours share A rows in that XCD's L2).
 constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64, G2_THREADS = 512;
 constexpr int G2_HALF = 128 * G2_BK;  // halves per half-tile (16 KB)
 constexpr int G2_LDS = 2 * 4 * G2_HALF * 2;  // bytes: 128 KB
@@ -313,7 +317,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
   mma(MH, NH, BB);                                     \
   __builtin_amdgcn_sched_barrier(0);
-  // prologue: tile 0 whole, tile 1's B halves in flight
+  // prologue: tile 0 whole, tile 1's B halves in flight (as if staged in P4 of tile -1)
   stage(0, 2);
   stage(0, 3);
   stage(0, 0);
@@ -322,6 +326,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   stage(1, 3);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   for (int t = 0; t < nk; ++t) {
     const int cb = t & 1;
     rdA(cb, 0);
@@ -334,15 +339,16 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     G2_SYNC_MMA(0, 1, b1)
     __builtin_amdgcn_s_barrier();
     rdA(cb, 1);
-    stage(t + 2, 2);
     G2_SYNC_MMA(1, 1, b1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B halves) landed
     __builtin_amdgcn_s_barrier();
+    stage(t + 2, 2);
     stage(t + 2, 3);
     G2_SYNC_MMA(1, 0, b0)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
 #undef G2_SYNC_MMA
+  if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
   // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
 #pragma unroll
