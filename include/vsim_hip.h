@@ -129,6 +129,12 @@ int vsim_op_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd
 int vsim_op_q4_expand_f16(const void *w, int M, int K, void *w16, void *stream);
 int vsim_op_gemm_f16(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *y,
                      void *stream);
+/* The activation step between two prompt GEMMs: x [n][K] f32 -> (x + bias, GELU table: when
+ * gelu != 0) -> quantize_row_q4_0 per 32-block -> the values d*(q-8) as fp16 [n][K].  And the
+ * fc_in GEMM with that step in its epilogue (q16 [n][M] instead of y; M % 32 == 0). */
+int vsim_op_act_quant_f16(const float *x, int K, int n, const float *bias, int gelu, void *x16, void *stream);
+int vsim_op_gemm_f16_gelu_q(const void *w16, int M, int K, const void *x16, int n, const float *bias, void *q16,
+                            void *stream);
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream);
 /* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);

@@ -287,6 +287,26 @@ def test_prefill_gemm_f16_256(M, K, N):
     assert not bad.any(), f"{bad.sum()} of {bad.size} outside the bound, first {np.argwhere(bad)[:4].tolist()}"
 
 
+@pytest.mark.parametrize("M,K,N", [(512, 256, 300), (1056, 128, 257), (4096, 1024, 512)])
+def test_prefill_gemm_gelu_epilogue_bit_identical(M, K, N):
+    """fc_in of a long prompt with bias + GELU + Q4_0 quantize in the GEMM epilogue gives the
+    same fp16 operand bits as the GEMM's f32 output through k_act_quant_f16 (ragged M, N)."""
+    rng = np.random.default_rng(M + 7 * K + N)
+    W16 = (rng.standard_normal((M, K)) * 0.05).astype(np.float16)
+    X16 = (rng.standard_normal((N, K)) * 0.5).astype(np.float16)
+    b = (rng.standard_normal(M) * 0.1).astype(np.float32)
+    w, x, bd = torch.from_numpy(W16).to(DEV), torch.from_numpy(X16).to(DEV), dev(b)
+    y = torch.empty(N * M, dtype=torch.float32, device=DEV)
+    ref = torch.empty(N * M, dtype=torch.float16, device=DEV)
+    got = torch.empty(N * M, dtype=torch.float16, device=DEV)
+    L = hip.lib()
+    hip.check(L.vsim_op_gemm_f16(w.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None), "gemm")
+    hip.check(L.vsim_op_act_quant_f16(y.data_ptr(), M, N, bd.data_ptr(), 1, ref.data_ptr(), None), "act")
+    hip.check(L.vsim_op_gemm_f16_gelu_q(w.data_ptr(), M, K, x.data_ptr(), N, bd.data_ptr(), got.data_ptr(), None), "gq")
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
 @pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])
 def test_attn_prefill_f16(d, H, N, n_past):
     """Fast-mode prompt attention (attn_prefill.hip) against fp64 causal attention:

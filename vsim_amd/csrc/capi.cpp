@@ -58,6 +58,15 @@ int vsim_op_gemm_f16(const void *w16, int M, int K, const void *x16, int n, cons
   if (!w16 || !x16 || !y) { set_error("gemm_f16: null argument"); return VSIM_EINVAL; }
   return launch_gemm_f16_256(w16, M, K, x16, n, bias, y, (hipStream_t)stream);
 }
+int vsim_op_act_quant_f16(const float *x, int K, int n, const float *bias, int gelu, void *x16, void *stream) {
+  if (!x || !x16) { set_error("act_quant_f16: null argument"); return VSIM_EINVAL; }
+  return launch_act_quant_f16(x, K, n, bias, gelu != 0, x16, (hipStream_t)stream);
+}
+int vsim_op_gemm_f16_gelu_q(const void *w16, int M, int K, const void *x16, int n, const float *bias, void *q16,
+                            void *stream) {
+  if (!w16 || !x16 || !q16) { set_error("gemm_f16_gelu_q: null argument"); return VSIM_EINVAL; }
+  return launch_gemm_f16_256(w16, M, K, x16, n, bias, nullptr, (hipStream_t)stream, q16);
+}
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream) {
   return launch_get_rows(w, K, V, rows, n, y, (hipStream_t)stream);
 }

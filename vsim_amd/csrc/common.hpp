@@ -262,8 +262,10 @@ int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, flo
 #endif
 constexpr int G2_MIN_N = VSIM_G2_MIN_N;
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
+// q16 non-null: y is not written; bias + GELU + Q4_0 quantize of the result into q16 ([n][M]
+// fp16 values d*(q-8), the next GEMM's operand, as launch_act_quant_f16(y, ..., gelu) makes)
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
-                        hipStream_t s);
+                        hipStream_t s, void *q16 = nullptr);
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call)

@@ -243,9 +243,16 @@ __global__ void __launch_bounds__(256) k_w4_expand_f16(W4 W, half8 *__restrict__
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// GQ: the fc_in epilogue of the next GEMM's operand instead of Y: bias + GELU table
+// (ggml.c:4113-4152) + quantize_row_q4_0 per 32 consecutive rows m + the values d*(q-8) as
+// fp16 into Q16[n][m] -- what k_act_quant_f16 makes of Y + bias, without Y's round trip.  A
+// 32-row block of one column n sits in 4 lanes (fk = 0..3) x 8 registers of two accumulators.
+template <bool GQ>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
                                                                  const _Float16 *__restrict__ B, int N,
-                                                                 const float *__restrict__ bias, float *__restrict__ Y) {
+                                                                 const float *__restrict__ bias, float *__restrict__ Y,
+                                                                 const uint16_t *__restrict__ gelu_tab,
+                                                                 _Float16 *__restrict__ Q16) {
   extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2, wc = wave & 3;
@@ -351,6 +358,46 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
   // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
+  if constexpr (GQ) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int mb = m0 + wr * 128 + 32 * p;  // the block's first row
+      float bv[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bv[e] = mb + 4 * fk + e < M ? bias[mb + 4 * fk + e] : 0.0f;
+        bv[4 + e] = mb + 16 + 4 * fk + e < M ? bias[mb + 16 + 4 * fk + e] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = h2f(gelu_tab[f2h(acc[2 * p][j][e] + bv[e])]);
+          v[4 + e] = h2f(gelu_tab[f2h(acc[2 * p + 1][j][e] + bv[4 + e])]);
+        }
+        float amax = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = amax > fabsf(v[e]) ? amax : fabsf(v[e]);
+        float o = __shfl_xor(amax, 16, 64);
+        amax = amax > o ? amax : o;
+        o = __shfl_xor(amax, 32, 64);
+        amax = amax > o ? amax : o;
+        const float d = amax / 7.0f;
+        const float id = d != 0.0f ? 1.0f / d : 0.0f;
+        _Float16 h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (_Float16)(d * (float)(x86_round_i8(v[e] * id)));
+        const int n = n0 + wc * 64 + j * 16 + fr;
+        if (n < N && mb < M) {
+          _Float16 *dst = Q16 + (size_t)n * M + mb + 4 * fk;
+          *(uint2 *)dst = *(const uint2 *)&h[0];
+          *(uint2 *)(dst + 16) = *(const uint2 *)&h[4];
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + i * 16 + 4 * fk;
@@ -384,19 +431,30 @@ int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s) {
 }
 
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
-                        hipStream_t s) {
-  if (K % G2_BK || K <= 0 || M <= 0 || n <= 0) {
-    set_error("f16 gemm: K must be a positive multiple of 64");
+                        hipStream_t s, void *q16) {
+  if (K % G2_BK || K <= 0 || M <= 0 || n <= 0 || (q16 && (M % QK || !bias))) {
+    set_error("f16 gemm: K must be a positive multiple of 64 (and M of 32, with a bias, for the GELU epilogue)");
     return VSIM_EINVAL;
   }
   static bool attr = false;
   if (!attr) {
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));
     attr = true;
   }
+  const uint16_t *tab = nullptr;
+  if (q16) {
+    DevTables t;
+    if (int rc = tables_get(&t)) return rc;
+    tab = t.gelu_f16;
+  }
   const int nwg = ((M + G2_BM - 1) / G2_BM) * ((n + G2_BN - 1) / G2_BN);
-  hipLaunchKernelGGL(k_gemm_f16_256, dim3(nwg), dim3(G2_THREADS), G2_LDS, s, (const _Float16 *)A16, M, K,
-                     (const _Float16 *)x16, n, bias, y);
+  if (q16)
+    hipLaunchKernelGGL(k_gemm_f16_256<true>, dim3(nwg), dim3(G2_THREADS), G2_LDS, s, (const _Float16 *)A16, M, K,
+                       (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16);
+  else
+    hipLaunchKernelGGL(k_gemm_f16_256<false>, dim3(nwg), dim3(G2_THREADS), G2_LDS, s, (const _Float16 *)A16, M, K,
+                       (const _Float16 *)x16, n, bias, y, nullptr, nullptr);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

@@ -489,8 +489,12 @@ double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 
 // Quantize an activation and run one GEMV in the model's mode.  x16 non-null (fast-mode
 // prompt batches): the activation is already the GEMM's fp16 operand (launch_act_quant_f16).
+// gq (fc_in of a long prompt): bias gq_bias + GELU + quantize of the product straight into the
+// next GEMM's fp16 operand gq, in the GEMM's epilogue; *fused tells the caller whether it ran.
 int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_t *xq, float *xd, bool quantize,
-       const float *bias, float *y, int &nk, const void *x16 = nullptr) {
+       const float *bias, float *y, int &nk, const void *x16 = nullptr, void *gq = nullptr,
+       const float *gq_bias = nullptr, bool *fused = nullptr) {
+  if (fused) *fused = false;
   if (quantize && !x16) {
     RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
     ++nk;
@@ -505,10 +509,12 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
       RC(launch_w4_expand_f16(w4_view(W, M, K), img, m->stream));
       ++nk;
     }
+    const bool gelu = gq && gq_bias && M % QK == 0;
     const long ev = prof_begin(m);
-    RC(launch_gemm_f16_256(img, M, K, x16, N, bias, y, m->stream));
+    RC(launch_gemm_f16_256(img, M, K, x16, N, gelu ? gq_bias : bias, y, m->stream, gelu ? gq : nullptr));
     prof_end(m, ev, "k_gemm_f16_256 (prompt)", (double)M * K / QK * QBYTES);
     ++nk;
+    if (fused) *fused = gelu;
     return VSIM_OK;
   }
   const long ev = prof_begin(m);
@@ -559,9 +565,10 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   RC(launch_add_bias(m->cur2, m->inpL, N * E, 1, s)); ++nk;
   RC(launch_norm(m->cur2, m->cur1, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
   RC(act16(m->cur1, E, xa, nullptr, false));
-  RC(mm(m, L.wfc, F, E, m->cur1, N, m->xq2, m->xd2, true, nullptr, m->fch, nk, xa));
+  bool gq = false;
+  RC(mm(m, L.wfc, F, E, m->cur1, N, m->xq2, m->xd2, true, nullptr, m->fch, nk, xa, xb, L.bfc, &gq));
   if (pf) {
-    RC(act16(m->fch, F, xb, L.bfc, true));  // bias + GELU + quantize, one pass
+    if (!gq) RC(act16(m->fch, F, xb, L.bfc, true));  // bias + GELU + quantize, one pass
   } else {
     RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
   }
@@ -641,9 +648,10 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
     fquant = true;
   }
   if (fquant) RC(act16(fx, E, X.a, nullptr, false));
-  RC(mm(m, L.wfc, F, E, fx, N, (uint8_t *)fxq, (float *)fxd, fquant, nullptr, m->fch, nk, X.a));
+  bool gq = false;
+  RC(mm(m, L.wfc, F, E, fx, N, (uint8_t *)fxq, (float *)fxd, fquant, nullptr, m->fch, nk, X.a, X.b, L.bfc, &gq));
   if (pf) {
-    RC(act16(m->fch, F, X.b, L.bfc, true));  // bias + GELU + quantize, one pass
+    if (!gq) RC(act16(m->fch, F, X.b, L.bfc, true));  // bias + GELU + quantize, one pass
   } else {
     RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
   }
