@@ -248,6 +248,9 @@ int launch_act_unpack(const void *xq, void *aos, int n, int k, hipStream_t s);
 int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s);
 int launch_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, hipStream_t s);
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s);
+// prompt batches: the norm + affine of each row straight to the GEMM's fp16 operand
+// (launch_act_quant_f16 of launch_norm's output, in one kernel)
+int launch_norm_f16q(const float *x, void *x16, int k, int rows, const float *w, const float *b, hipStream_t s);
 int launch_argmax(const float *x, int n, int *out, hipStream_t s);
 int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s);
 // fast-mode prompt batches (n >= GEMM_MIN_N): activation rows quantized (optionally after

@@ -177,10 +177,12 @@ namespace vsim {
 // residual graphs, vsim.cpp:628, 659 and BLOOM): v = x + (ja + jab) or v = x + (jf + jfb);
 // written to jout when jout != null.
 // stats (optional): [0] mean fallbacks, [1] variance fallbacks.
+// CERT = false (fast-mode prompt batches only): the tree sums are used as they are, without
+// the certificate and its sequential fallbacks (a fallback row costs one lane ~25-50 us).
 // n % 4 == 0; float4 accesses, NT threads x 4 elements per pass, so for n <= 4*NT every load
 // of a pass issues at once (a loop of scalar loads behind branches serialized on their
 // latency and dominated the kernel).
-template <int NT>
+template <int NT, bool CERT = true>
 __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
                                const float *__restrict__ gb, unsigned *stats, const float *__restrict__ ja = nullptr,
                                const float *__restrict__ jab = nullptr, const float *__restrict__ jf = nullptr,
@@ -266,7 +268,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
     sa += shsa[w];
     um = min(um, shu[w]);
   }
-  const bool exact = (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
+  const bool exact = !CERT || (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
   if (!exact) {
     // sequential fallback, 4 independent partial loads per step to keep the LDS reads ahead
     if (threadIdx.x == 0) {
@@ -306,7 +308,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
   const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
   float scale = sc_lo;
-  if (sc_lo != sc_hi) {
+  if (CERT && sc_lo != sc_hi) {
     if (threadIdx.x == 0) {
       double q = 0.0;
       for (int i = 0; i < n; ++i) {

@@ -545,8 +545,12 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
     ++nk;
     return launch_act_quant_f16(x, K, N, gbias, gelu, x16, s);
   };
-  RC(launch_norm(m->inpL, m->cur1, E, N, L.ln1_w, L.ln1_b, s)); ++nk;
-  RC(act16(m->cur1, E, xa, nullptr, false));
+  // LayerNorm (straight to the GEMM's fp16 operand in a prompt batch)
+  auto norm = [&](const float *x, float *y, const float *w, const float *b, void *x16) -> int {
+    ++nk;
+    return pf ? launch_norm_f16q(x, x16, E, N, w, b, s) : launch_norm(x, y, E, N, w, b, s);
+  };
+  RC(norm(m->inpL, m->cur1, L.ln1_w, L.ln1_b, xa));
   RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, L.bq, m->Qb, nk, xa));
   RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bk, m->Kb, nk, xa));
   RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, L.bv, m->Vb, nk, xa));
@@ -563,8 +567,7 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   // inpFF = attn + inpL (kept in cur2), its LayerNorm into cur1
   VSIM_HIP(hipMemcpyAsync(m->cur2, m->attn, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
   RC(launch_add_bias(m->cur2, m->inpL, N * E, 1, s)); ++nk;
-  RC(launch_norm(m->cur2, m->cur1, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
-  RC(act16(m->cur1, E, xa, nullptr, false));
+  RC(norm(m->cur2, m->cur1, L.ln2_w, L.ln2_b, xa));
   bool gq = false;
   RC(mm(m, L.wfc, F, E, m->cur1, N, m->xq2, m->xd2, true, nullptr, m->fch, nk, xa, xb, L.bfc, &gq));
   if (pf) {
@@ -600,8 +603,11 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
     return launch_act_quant_f16(x, K, N, gbias, gelu, x16, s);
   };
   // input LayerNorm + affine (vsim.cpp:526-533)
-  RC(launch_norm(m->inpL, m->cur1, E, N, L.ln1_w, L.ln1_b, s)); ++nk;
-  RC(act16(m->cur1, E, X.a, nullptr, false));
+  auto norm = [&](const float *x, float *y, const float *w, const float *b, void *x16) -> int {
+    ++nk;  // (prompt batch: straight to the GEMM's fp16 operand)
+    return pf ? launch_norm_f16q(x, x16, E, N, w, b, s) : launch_norm(x, y, E, N, w, b, s);
+  };
+  RC(norm(m->inpL, m->cur1, L.ln1_w, L.ln1_b, X.a));
   // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
   RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a));
   RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, m->Kb, nk, X.a));
@@ -635,19 +641,19 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   const float *fx = m->cur1;
   if (!gptj) {
     if (m->hp.use_parallel_residual) {
-      RC(launch_norm(m->inpL, m->cur2, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
+      RC(norm(m->inpL, m->cur2, L.ln2_w, L.ln2_b, X.a));
     } else {
       // inpFF = cur + inpL ; norm ; affine  (vsim.cpp:631-649)
       VSIM_HIP(hipMemcpyAsync(m->cur2, m->attn, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
       RC(launch_add_bias(m->cur2, m->inpL, N * E, 1, s)); ++nk;  // cur + inpL elementwise
-      RC(launch_norm(m->cur2, m->cur2, E, N, L.ln2_w, L.ln2_b, s)); ++nk;
+      RC(norm(m->cur2, m->cur2, L.ln2_w, L.ln2_b, X.a));
     }
     fx = m->cur2;
     fxq = m->xq2;
     fxd = m->xd2;
     fquant = true;
   }
-  if (fquant) RC(act16(fx, E, X.a, nullptr, false));
+  // (the norms above wrote the prompt batch's fp16 operand already)
   bool gq = false;
   RC(mm(m, L.wfc, F, E, fx, N, (uint8_t *)fxq, (float *)fxd, fquant, nullptr, m->fch, nk, X.a, X.b, L.bfc, &gq));
   if (pf) {

@@ -31,6 +31,29 @@ __global__ void __launch_bounds__(NORM_THREADS) k_norm_exact(const float *__rest
   for (int i = threadIdx.x; i < n; i += NORM_THREADS) y[i] = xrow[i];
 }
 
+// Fast-mode prompt LayerNorm straight to the next GEMM's fp16 operand: the norm + affine of
+// one row in LDS (double tree sums, without the exact path's certificate and sequential
+// fallbacks: ~3 % of rows, each ~25-50 us of one lane, set this kernel's time), then
+// quantize_row_q4_0 per 32-block and the values d*(q-8) as fp16.
+// 512 threads: rows up to 8192 take the norm's all-loads-at-once path (4 float4 per thread)
+constexpr int NORMQ_THREADS = 512;
+__global__ void __launch_bounds__(NORMQ_THREADS) k_norm_f16q(const float *__restrict__ X, _Float16 *__restrict__ Q16,
+                                                             int n, const float *__restrict__ gw,
+                                                             const float *__restrict__ gb, unsigned *stats) {
+  extern __shared__ __attribute__((aligned(16))) float xrow[];
+  ln_exact_lds_t<NORMQ_THREADS, false>(X + (size_t)blockIdx.x * n, xrow, n, gw, gb, stats);
+  const int lane = threadIdx.x & 63, nb = n / QK;
+  _Float16 *q = Q16 + (size_t)blockIdx.x * n;
+  for (int b2 = threadIdx.x >> 6; 2 * b2 < nb; b2 += NORMQ_THREADS / 64) {
+    const int b = 2 * b2 + (lane >> 5);
+    const bool ok = b < nb;  // (uniform per half-wave)
+    const float v = ok ? xrow[b * QK + (lane & 31)] : 0.0f;
+    float d;
+    const int qv = q4_half(v, d);
+    if (ok) q[b * QK + (lane & 31)] = (_Float16)(d * (float)(qv - 8));
+  }
+}
+
 unsigned *g_norm_stats = nullptr;  // device counters of LayerNorm fallbacks (ln_exact_lds)
 
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s) {
@@ -38,6 +61,15 @@ int launch_norm(const float *x, float *y, int k, int rows, const float *w, const
   if ((w == nullptr) != (b == nullptr)) { set_error("norm: affine needs both w and b"); return VSIM_EINVAL; }
   if ((size_t)k * 4 > 64 * 1024) { set_error("norm: row longer than 16384"); return VSIM_EINVAL; }
   hipLaunchKernelGGL(k_norm_exact, dim3(rows), dim3(NORM_THREADS), (size_t)k * 4, s, x, y, k, w, b, g_norm_stats);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+int launch_norm_f16q(const float *x, void *x16, int k, int rows, const float *w, const float *b, hipStream_t s) {
+  if (k <= 0 || rows <= 0 || k % QK || !w || !b) { set_error("norm_f16q: bad shape"); return VSIM_EINVAL; }
+  if ((size_t)k * 4 > 64 * 1024) { set_error("norm: row longer than 16384"); return VSIM_EINVAL; }
+  hipLaunchKernelGGL(k_norm_f16q, dim3(rows), dim3(NORMQ_THREADS), (size_t)k * 4, s, x, (_Float16 *)x16, k, w, b,
+                     g_norm_stats);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
