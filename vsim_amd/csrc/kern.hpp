@@ -182,7 +182,7 @@ namespace vsim {
 // n % 4 == 0; float4 accesses, NT threads x 4 elements per pass, so for n <= 4*NT every load
 // of a pass issues at once (a loop of scalar loads behind branches serialized on their
 // latency and dominated the kernel).
-template <int NT, bool CERT = true>
+template <int NT, bool CERT = true, int UP = 4>
 __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, const float *__restrict__ gw,
                                const float *__restrict__ gb, unsigned *stats, const float *__restrict__ ja = nullptr,
                                const float *__restrict__ jab = nullptr, const float *__restrict__ jf = nullptr,
@@ -227,7 +227,7 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   auto ld4 = [](const float *p, int i) {
     return p ? ((const float4 *)p)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  constexpr int UP = 4;  // rows up to UP * NT float4: every load issued before any arithmetic
+  // rows up to UP * NT float4: every load issued before any arithmetic
   if (n4 <= UP * NT) {
     float4 v[UP], a[UP], ab[UP], f[UP], fb[UP];
 #pragma unroll
