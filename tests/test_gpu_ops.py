@@ -257,13 +257,14 @@ def test_prefill_gemm_f16(M, K, N):
 
 
 @pytest.mark.parametrize("M,K,N", [(520, 512, 300), (256, 64, 256), (1000, 128, 600), (3072, 1024, 512),
-                                   (300, 4096, 257)])
+                                   (300, 4096, 257), (24576, 64, 2048)])
 def test_prefill_gemm_f16_256(M, K, N):
     """Long-prompt GEMM (gemm_f16.hip k_gemm_f16_256 on the fp16 weight image of
     k_w4_expand_f16): the image holds exactly the fp16 roundings of d*(q-8); the product is
     within 4*K*2^-24*sum|w16*x16| of the fp64 product of the same fp16 operands.  Ragged M
-    and N (not multiples of the 256 x 256 tile), K = 64 and 128 (one and two K-tiles: the
-    prologue's and loop's clamped stages), K = 4096."""
+    and N (not multiples of the tile), K = 64 and 128 (one and two K-tiles: the prologue's and
+    loop's clamped stages), K = 4096; 192-row tiles everywhere but (24576, 64, 2048), whose
+    shape takes the 256-row tiles (launch_gemm_f16_256's choice)."""
     rng = np.random.default_rng(3 * M + K + N)
     w_aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05))
     b = rng.standard_normal(M).astype(np.float32)

@@ -205,29 +205,31 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16
 // (k_w4_expand_f16: the same halves deq_block_f16 gives), kept by the model per weight, so the
 // GEMM stages both operands by LDS-DMA straight from HBM/L2 and the K loop carries no dequant.
 //
-// k_gemm_f16_256: one 512-thread workgroup per 256 x 256 output tile (8 waves: 2 along M x 4
-// along N, 128 x 64 each, v_mfma_f32_16x16x32_f16, 32 accumulators of 4), K in tiles of 64.
-// LDS: two buffers x {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255} of 16 KB
-// ("half-tiles", [128 rows][64 halves], 16-byte chunks XOR-swizzled by (row >> 1) & 7 so the
-// 16 lanes of a ds_read_b128 group hit 16 different bank slots).  Each K-tile is 4 phases, one
-// output quadrant (64 x 32 per wave, 16 MFMAs) per phase; a phase is {LDS reads, DMA issue}
-// barrier {MFMAs} barrier.  The two wave groups (waves 0-3: A rows 0-127, waves 4-7: rows
-// 128-255; one of each per SIMD) run one barrier apart, so on every SIMD one wave's MFMAs
-// overlap the other's LDS reads (group 1 takes one extra barrier first, group 0 one last):
-//   P1: read A rows 0-63 + B cols 0-31, stage A h0 of tile t+1
-//   P2: read B cols 32-63,             stage A h1 of tile t+1
-//   P3: read A rows 64-127,            wait for all of tile t+1 (vmcnt(0))
-//   P4: (B cols 0-31 still held),      stage B h0 and B h1 of tile t+2
-// With the groups a barrier apart, a half-tile is restaged >= 2 phases after its last read (A
-// halves: read up to P3, restaged in P1/P2 of the next tile; B halves: read up to P2, restaged
-// in P4) and read >= 2 phases after the wait that retires it (tile t+1 waited in P3 of tile t,
-// first read in P1 of tile t+1) -- cdna_hip_programming.md §5 ("read a staged buffer one
-// phase after the wait", "one barrier more when two wave groups run staggered").  The DMA
-// stays in flight across the raw s_barriers.  Workgroups are remapped so each XCD takes a
-// contiguous range of tiles (neighbours share A rows in that XCD's L2).
-constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64, G2_THREADS = 512;
-constexpr int G2_HALF = 128 * G2_BK;  // halves per half-tile (16 KB)
-constexpr int G2_LDS = 2 * 4 * G2_HALF * 2;  // bytes: 128 KB
+// k_gemm_f16_256: one 512-thread workgroup per BM x 256 output tile, BM = 64 * AP (AP = 4:
+// 256 rows, AP = 3: 192 rows, chosen per shape so the tiles fill the 256 CUs: M = 6144 at
+// N = 2048 is 192 tiles of 256 rows but 256 tiles of 192), 8 waves: 2 along M x 4 along N,
+// (BM/2) x 64 each, v_mfma_f32_16x16x32_f16, K in tiles of 64.  LDS: two buffers x {AP A
+// pieces, 4 B pieces} of 8 KB ([64 rows][64 halves], 16-byte chunks XOR-swizzled by
+// (row >> 1) & 7 so the 16 lanes of a ds_read_b128 group hit 16 different bank slots; the DMA
+// is lane-linear, the swizzle is on its source address).  Each K-tile is 4 phases, one output
+// quadrant ((BM/4) x 32 per wave) per phase; a phase is {LDS reads, DMA issue} barrier {MFMAs}
+// barrier.  The two wave groups (A rows [0, BM/2) and [BM/2, BM); one wave of each per SIMD)
+// run one barrier apart, so on every SIMD one wave's MFMAs overlap the other's LDS reads
+// (group 1 takes one extra barrier first, group 0 one last):
+//   P1: read A rows 0..BM/4-1 of the wave's half + B cols 0-31, stage A pieces [0, AP/2) of t+1
+//   P2: read B cols 32-63,                                     stage A pieces [AP/2, AP) of t+1
+//   P3: read A rows BM/4..BM/2-1,                              wait for all of tile t+1 (vmcnt(0))
+//   P4: (B cols 0-31 still held),                              stage the 4 B pieces of tile t+2
+// With the groups a barrier apart, a piece is restaged >= 2 phases after its last read (A:
+// read up to P3, restaged in P1/P2 of the next tile; B: read up to P2, restaged in P4) and read
+// >= 2 phases after the wait that retires it (tile t+1 waited in P3 of tile t, first read in P1
+// of tile t+1) -- cdna_hip_programming.md §5 ("read a staged buffer one phase after the wait",
+// "one barrier more when two wave groups run staggered").  The DMA stays in flight across the
+// raw s_barriers.  Workgroups are remapped so each XCD takes a contiguous range of tiles
+// (neighbours share A rows in that XCD's L2).
+constexpr int G2_BN = 256, G2_BK = 64, G2_THREADS = 512;
+constexpr int G2_PIECE = 64 * G2_BK;  // halves per staged piece (8 KB)
+__host__ __device__ constexpr int g2_lds_bytes(int ap) { return 2 * (ap + 4) * G2_PIECE * 2; }
 
 __global__ void __launch_bounds__(256) k_w4_expand_f16(W4 W, half8 *__restrict__ out) {
   const int nb = W.k / QK;
@@ -247,75 +249,71 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // (ggml.c:4113-4152) + quantize_row_q4_0 per 32 consecutive rows m + the values d*(q-8) as
 // fp16 into Q16[n][m] -- what k_act_quant_f16 makes of Y + bias, without Y's round trip.  A
 // 32-row block of one column n sits in 4 lanes (fk = 0..3) x 8 registers of two accumulators.
-template <bool GQ>
+template <bool GQ, int AP>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
                                                                  const _Float16 *__restrict__ B, int N,
                                                                  const float *__restrict__ bias, float *__restrict__ Y,
                                                                  const uint16_t *__restrict__ gelu_tab,
                                                                  _Float16 *__restrict__ Q16) {
+  constexpr int BM = 64 * AP, MR = 2 * AP;  // tile rows; 16-row M-reps per wave
+  constexpr int NPC = AP + 4;               // pieces per buffer
   extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2, wc = wave & 3;
-  const int tm = (M + G2_BM - 1) / G2_BM, tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
+  const int tm = (M + BM - 1) / BM, tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
   // XCD remap (bijective): the blocks dispatched to one XCD (bid % 8) take consecutive tiles
   const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int m0 = (wg / tn) * G2_BM, n0 = (wg % tn) * G2_BN;
+  const int m0 = (wg / tn) * BM, n0 = (wg % tn) * G2_BN;
   const int nk = K / G2_BK;
   const uint32_t lbase = lds_addr(g2lds);
-  // stage half-tile `part` (0/1: A rows h*128.., 2/3: B rows) of K-tile kt into buffer kt & 1;
-  // the source tile is clamped to the last one (the loads past the end fill a buffer that is
-  // not read again, and keep the per-wave DMA count of every phase the same)
-  auto stage = [&](int kt, int part) {
+  // stage piece p (A: p < AP, rows 64p..; B: p - AP) of K-tile kt into buffer kt & 1; the
+  // source tile is clamped to the last one (the loads past the end fill a buffer that is not
+  // read again, and keep the per-wave DMA count of every phase the same)
+  auto stage = [&](int kt, int p) {
     const int kc = min(kt, nk - 1);
-    const bool isA = part < 2;
-    const int h = part & 1;
-    const _Float16 *src = isA ? A : B;
-    const int lim = (isA ? M : N) - 1, r00 = (isA ? m0 : n0) + h * 128;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int rb = (j * 8 + wave) * 8;      // first row (within the half) of this instruction
-      const int r = rb + (lane >> 3);         // this lane's row
-      const int c = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at LDS chunk lane & 7
-      const _Float16 *g = src + (size_t)min(r00 + r, lim) * K + (size_t)kc * G2_BK + 8 * c;
-      glds16<false>(g, lbase + (uint32_t)((((kt & 1) * 4 + part) * G2_HALF + rb * G2_BK) * 2));
-    }
+    const bool isA = p < AP;
+    const int r = wave * 8 + (lane >> 3);        // this lane's row within the piece
+    const int c = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at LDS chunk lane & 7
+    const int grow = min((isA ? m0 + p * 64 : n0 + (p - AP) * 64) + r, (isA ? M : N) - 1);
+    const _Float16 *g = (isA ? A : B) + (size_t)grow * K + (size_t)kc * G2_BK + 8 * c;
+    glds16<false>(g, lbase + (uint32_t)((((kt & 1) * NPC + p) * G2_PIECE + wave * 8 * G2_BK) * 2));
   };
-  f32x4 acc[8][4];
+  f32x4 acc[MR][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MR; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  half8 a[4][2], b0[2][2], b1[2][2];
+  half8 a[AP][2], b0[2][2], b1[2][2];
   const int fr = lane & 15, fk = lane >> 4;
-  auto rd = [&](const _Float16 *half, int row, int kk) {  // fragment: 8 halves of `row` at k 8*fk + 32*kk
+  auto rd = [&](const _Float16 *base, int row, int kk) {  // fragment: 8 halves of `row` at k 8*fk + 32*kk
     const int c = kk * 4 + fk;
-    return *(const half8 *)(half + row * G2_BK + 8 * (c ^ ((row >> 1) & 7)));
+    return *(const half8 *)(base + row * G2_BK + 8 * (c ^ ((row >> 1) & 7)));
   };
-  auto rdA = [&](int buf, int mh) {
-    const _Float16 *hp = g2lds + (buf * 4 + wr) * G2_HALF;
+  auto rdA = [&](int buf, int mh) {  // rows of the tile: wave half wr, quarter mh
+    const _Float16 *bp = g2lds + buf * NPC * G2_PIECE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < AP; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[i][kk] = rd(hp, (4 * mh + i) * 16 + fr, kk);
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = rd(bp, wr * (BM / 2) + mh * (BM / 4) + i * 16 + fr, kk);
   };
   auto rdB = [&](half8 (&bb)[2][2], int buf, int nh) {
-    const _Float16 *hp = g2lds + (buf * 4 + 2 + (wc >> 1)) * G2_HALF;
+    const _Float16 *bp = g2lds + (buf * NPC + AP) * G2_PIECE;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bb[j][kk] = rd(hp, (wc & 1) * 64 + (2 * nh + j) * 16 + fr, kk);
+      for (int kk = 0; kk < 2; ++kk) bb[j][kk] = rd(bp, wc * 64 + (2 * nh + j) * 16 + fr, kk);
   };
   auto mma = [&](int mh, int nh, const half8 (&bb)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < AP; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[4 * mh + i][2 * nh + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][kk], bb[j][kk], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+          acc[AP * mh + i][2 * nh + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][kk], bb[j][kk], acc[AP * mh + i][2 * nh + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 #define G2_SYNC_MMA(MH, NH, BB)                        \
@@ -324,13 +322,13 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
   mma(MH, NH, BB);                                     \
   __builtin_amdgcn_sched_barrier(0);
-  // prologue: tile 0 whole, tile 1's B halves in flight (as if staged in P4 of tile -1)
-  stage(0, 2);
-  stage(0, 3);
-  stage(0, 0);
-  stage(0, 1);
-  stage(1, 2);
-  stage(1, 3);
+  // prologue: tile 0 whole, tile 1's B pieces in flight (as if staged in P4 of tile -1)
+#pragma unroll
+  for (int p = AP; p < NPC; ++p) stage(0, p);
+#pragma unroll
+  for (int p = 0; p < AP; ++p) stage(0, p);
+#pragma unroll
+  for (int p = AP; p < NPC; ++p) stage(1, p);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
@@ -338,19 +336,21 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     const int cb = t & 1;
     rdA(cb, 0);
     rdB(b0, cb, 0);
-    stage(t + 1, 0);
+#pragma unroll
+    for (int p = 0; p < AP / 2; ++p) stage(t + 1, p);
     G2_SYNC_MMA(0, 0, b0)
     __builtin_amdgcn_s_barrier();
     rdB(b1, cb, 1);
-    stage(t + 1, 1);
+#pragma unroll
+    for (int p = AP / 2; p < AP; ++p) stage(t + 1, p);
     G2_SYNC_MMA(0, 1, b1)
     __builtin_amdgcn_s_barrier();
     rdA(cb, 1);
     G2_SYNC_MMA(1, 1, b1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B halves) landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B pieces) landed
     __builtin_amdgcn_s_barrier();
-    stage(t + 2, 2);
-    stage(t + 2, 3);
+#pragma unroll
+    for (int p = AP; p < NPC; ++p) stage(t + 2, p);
     G2_SYNC_MMA(1, 0, b0)
     __builtin_amdgcn_s_barrier();
   }
@@ -358,10 +358,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
   // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
+  const int mw = m0 + wr * (BM / 2);  // the wave's first row
   if constexpr (GQ) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int mb = m0 + wr * 128 + 32 * p;  // the block's first row
+    for (int p = 0; p < AP; ++p) {
+      const int mb = mw + 32 * p;  // the block's first row
       float bv[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -399,8 +400,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     return;
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + 4 * fk;
+  for (int i = 0; i < MR; ++i) {
+    const int m = mw + i * 16 + 4 * fk;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (bias) {
 #pragma unroll
@@ -430,17 +431,44 @@ int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s) {
   return VSIM_OK;
 }
 
+// AP (tile height 64 * AP): the one of 3 and 4 whose tiles fill the CUs in fewer
+// tile-height-weighted rounds (ties: 4)
+static int g2_ap(int M, int n) {
+  const int cus = 256;
+  auto cost = [&](int ap) {
+    const long tiles = (long)((M + 64 * ap - 1) / (64 * ap)) * ((n + G2_BN - 1) / G2_BN);
+    return ((tiles + cus - 1) / cus) * ap;
+  };
+  return cost(3) < cost(4) ? 3 : 4;
+}
+
+template <int AP>
+static int g2_launch(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                     hipStream_t s, const uint16_t *tab, void *q16) {
+  static bool attr = false;
+  if (!attr) {
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<false, AP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 g2_lds_bytes(AP)));
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<true, AP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 g2_lds_bytes(AP)));
+    attr = true;
+  }
+  const int nwg = ((M + 64 * AP - 1) / (64 * AP)) * ((n + G2_BN - 1) / G2_BN);
+  if (q16)
+    hipLaunchKernelGGL((k_gemm_f16_256<true, AP>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s,
+                       (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16);
+  else
+    hipLaunchKernelGGL((k_gemm_f16_256<false, AP>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s,
+                       (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, nullptr, nullptr);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
                         hipStream_t s, void *q16) {
   if (K % G2_BK || K <= 0 || M <= 0 || n <= 0 || (q16 && (M % QK || !bias))) {
     set_error("f16 gemm: K must be a positive multiple of 64 (and M of 32, with a bias, for the GELU epilogue)");
     return VSIM_EINVAL;
-  }
-  static bool attr = false;
-  if (!attr) {
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));
-    attr = true;
   }
   const uint16_t *tab = nullptr;
   if (q16) {
@@ -448,15 +476,8 @@ int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, c
     if (int rc = tables_get(&t)) return rc;
     tab = t.gelu_f16;
   }
-  const int nwg = ((M + G2_BM - 1) / G2_BM) * ((n + G2_BN - 1) / G2_BN);
-  if (q16)
-    hipLaunchKernelGGL(k_gemm_f16_256<true>, dim3(nwg), dim3(G2_THREADS), G2_LDS, s, (const _Float16 *)A16, M, K,
-                       (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16);
-  else
-    hipLaunchKernelGGL(k_gemm_f16_256<false>, dim3(nwg), dim3(G2_THREADS), G2_LDS, s, (const _Float16 *)A16, M, K,
-                       (const _Float16 *)x16, n, bias, y, nullptr, nullptr);
-  VSIM_HIP(hipGetLastError());
-  return VSIM_OK;
+  return g2_ap(M, n) == 3 ? g2_launch<3>(A16, M, K, x16, n, bias, y, s, tab, q16)
+                          : g2_launch<4>(A16, M, K, x16, n, bias, y, s, tab, q16);
 }
 
 int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s) {
