@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 o=gpurun_out
 mkdir -p $o
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 120 --timeout-method thread -k "gemm or quant" > $o/g256_ops.log 2>&1 || { tail -30 $o/g256_ops.log; exit 1; }
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 120 --timeout-method thread -k "gemm or quant or attn_prefill" > $o/g256_ops.log 2>&1 || { tail -30 $o/g256_ops.log; exit 1; }
 tail -1 $o/g256_ops.log
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_prefill.py tests/test_gpu_model.py -m gpu -x -q -s --timeout 300 --timeout-method thread -k "prompt or prefill or poison" > $o/g256_prefill.log 2>&1 || { tail -30 $o/g256_prefill.log; exit 1; }
 grep -E "cos|passed|failed" $o/g256_prefill.log | tail -12

@@ -149,9 +149,37 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
       *(u32x4 *)&Vt[(c8 / 8) * VLD + 8 * (c8 % 8)] = rv[c];
     }
   };
-  // D = 256: one LDS buffer, the tile staged at the top of each step (the register ring of
-  // the next tile does not fit beside the 256-dim Q fragments and O^T accumulators)
-  constexpr bool PF = D < 256;
+  // D = 256 (GL): the register ring of the next tile does not fit beside the 256-dim Q
+  // fragments and O^T accumulators, so the tiles go by LDS-DMA into two unpadded LDS buffers
+  // (16-byte chunks XOR-swizzled on the DMA's source address: K rows by row & 15, V^T rows by
+  // (row >> 1) & 7), the next tile in flight during this one's MFMAs; retired by vmcnt(0) before
+  // the step's closing barrier.
+  constexpr bool GL = D == 256;
+  constexpr bool PF = !GL;
+  const uint32_t lb = lds_addr(lds);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);  // (the DMA's LDS address goes to M0)
+  auto gl_stage = [&](int kb, int buf) __attribute__((always_inline)) {
+    const int k0 = kb * AP_BK;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // K: 2 rows (keys) per wave instruction
+      const int row0 = (j * 4 + wv) * 2, row = row0 + (lane >> 5);
+      const int c = (lane & 31) ^ (row & 15);
+      glds16<false>(kbase + (size_t)min(k0 + row, klast) * E + 8 * c,
+                    lb + (uint32_t)((buf * AP_BK * D + row0 * D) * 2));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // V^T: 8 rows (dims) per wave instruction
+      const int row0 = (j * 4 + wv) * 8, row = row0 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      glds16<false>(vbase + (size_t)row * ldt + k0 + 8 * c,
+                    lb + (uint32_t)((2 * AP_BK * D + buf * D * AP_BK + row0 * AP_BK) * 2));
+    }
+  };
+  if (GL) {
+    gl_stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   if (PF) {
     kload(0);
     vload(0);
@@ -160,18 +188,13 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
     __syncthreads();
   }
   for (int kb = 0; kb < nkb; ++kb) {
-    const int k0 = kb * AP_BK, buf = PF ? kb & 1 : 0;
+    const int k0 = kb * AP_BK, buf = kb & 1;
     const bool next = PF && kb + 1 < nkb;
-    if (!PF) {
-      kload(kb);
-      vload(kb);
-      kstore(0);
-      vstore(0);
-      __syncthreads();
-    }
+    if (GL && kb + 1 < nkb) gl_stage(kb + 1, buf ^ 1);
     // next tile: K rows load during this tile's S^T, V^T rows during its P·V
     if (next) kload(kb + 1);
-    const _Float16 *Ks = lds + buf * AP_BK * KLD, *Vt = lds + 2 * AP_BK * KLD + buf * D * VLD;
+    const _Float16 *Ks = GL ? lds + buf * AP_BK * D : lds + buf * AP_BK * KLD;
+    const _Float16 *Vt = GL ? lds + 2 * AP_BK * D + buf * D * AP_BK : lds + 2 * AP_BK * KLD + buf * D * VLD;
     const bool vis = k0 <= n_past + min(qw + 31, N - 1);  // wave-uniform: some key of the block is visible
     af32x16 st[2];
     if (vis) {
@@ -181,7 +204,9 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
         st[t] = (af32x16){};
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          const ahalf8 kf = *(const ahalf8 *)&Ks[(32 * t + r) * KLD + 16 * s + 8 * hl];
+          const int krow = 32 * t + r;
+          const ahalf8 kf = GL ? *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))]
+                               : *(const ahalf8 *)&Ks[krow * KLD + 16 * s + 8 * hl];
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st[t], 0, 0, 0);
           // (a scheduling fence every 4 steps: the compiler would otherwise hoist all the
           // tile's LDS reads and run out of registers at D = 256)
@@ -232,8 +257,10 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
           const int kbase2 = 32 * t + 16 * s2 + 4 * hl;
 #pragma unroll
           for (int i = 0; i < NT; ++i) {
-            const _Float16 *vr = &Vt[(32 * i + r) * VLD + kbase2];
-            const ahalf4 v0 = *(const ahalf4 *)vr, v1 = *(const ahalf4 *)(vr + 8);
+            const int vrow = 32 * i + r, vc = kbase2 >> 3;  // (kbase2 & 7 == 4 hl: within the chunk)
+            const _Float16 *vr = GL ? &Vt[vrow * AP_BK + 8 * (vc ^ ((vrow >> 1) & 7)) + 4 * hl] : &Vt[vrow * VLD + kbase2];
+            const _Float16 *vr1 = GL ? &Vt[vrow * AP_BK + 8 * ((vc + 1) ^ ((vrow >> 1) & 7)) + 4 * hl] : vr + 8;
+            const ahalf4 v0 = *(const ahalf4 *)vr, v1 = *(const ahalf4 *)vr1;
             const ahalf8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
             o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
             if (D >= 256 && (i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
@@ -241,6 +268,7 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
         }
     }
     if (next) vstore(buf ^ 1);
+    if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile has landed
     __syncthreads();
   }
   // O^T / l: lane = query, rows = dims (reg & 3) + 8 (reg >> 2) + 4 hl of tile i
@@ -262,8 +290,8 @@ bool attn_prefill_supported(int d) { return d == 64 || d == 96 || d == 128 || d 
 
 template <int D>
 size_t attn_prefill_lds() {
-  const int nbuf = D < 256 ? 2 : 1;
-  return (size_t)(2 * AP_BK * (D + 8) + nbuf * D * (AP_BK + 8)) * sizeof(_Float16);
+  if (D == 256) return (size_t)2 * 2 * AP_BK * D * sizeof(_Float16);  // K and V^T, two buffers each, unpadded
+  return (size_t)(2 * AP_BK * (D + 8) + 2 * D * (AP_BK + 8)) * sizeof(_Float16);
 }
 
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
@@ -286,6 +314,12 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
   hipLaunchKernelGGL(k_kv_f16, dim3(ldt / 64, E / 64), dim3(256), 0, s, kc, vc, E, d, nk, ldt, k16, vt16);
   const float qscale = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
   const dim3 grid(((N + AP_BQ - 1) / AP_BQ) * H);
+  static bool attr = false;
+  if (!attr) {
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_attn_prefill_f16<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)attn_prefill_lds<256>()));
+    attr = true;
+  }
 #define APL(DD)                                                                                                   \
   hipLaunchKernelGGL(k_attn_prefill_f16<DD>, grid, dim3(AP_THREADS), attn_prefill_lds<DD>(), s, Q, k16, vt16, E, H, \
                      N, n_past, ldt, qscale, out)
