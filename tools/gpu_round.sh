@@ -14,6 +14,8 @@ timeout -k 10 400 python3 "$root/bench.py" > "$out/bench_default_$tag.log" 2>&1
 fatal $? bench; tail -1 "$out/bench_default_$tag.log"
 timeout -k 10 300 python3 "$root/bench.py" --config codegen-16B --prefill 2048 --steps 3 > "$out/bench_prefill_$tag.log" 2>&1
 fatal $? prefill; tail -1 "$out/bench_prefill_$tag.log"
+timeout -k 10 300 python3 "$root/bench.py" --config bloom-560m --steps 128 --no-cpu-baseline > "$out/bench_bloom_$tag.log" 2>&1
+fatal $? bloom; tail -1 "$out/bench_bloom_$tag.log" | cut -c1-200
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_exact_$tag" -o run --output-format csv -- \
   python3 "$root/bench.py" --steps 64 --warmup 4 --no-cpu-baseline --no-fast --no-profile > "$out/prof_exact_$tag.log" 2>&1
 fatal $? prof_exact
