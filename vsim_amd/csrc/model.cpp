@@ -500,15 +500,25 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
     ++nk;
   }
   if (x16 && N >= G2_MIN_N && K % 64 == 0) {
-    // long prompt: the 256 x 256-tile GEMM on the weight's fp16 image
-    void *&img = m->w16[W];
+    // long prompt: the 256-wide-tile GEMM on the weight's fp16 image (made on first use)
+    auto it = m->w16.find(W);
+    void *img = it == m->w16.end() ? nullptr : it->second;
     if (!img) {
       const size_t bytes = (size_t)M * K * sizeof(uint16_t);
-      VSIM_HIP(hipMalloc(&img, bytes));
-      m->w16_bytes += bytes;
-      RC(launch_w4_expand_f16(w4_view(W, M, K), img, m->stream));
-      ++nk;
+      if (hipMalloc(&img, bytes) != hipSuccess) {
+        // no room for the image: this GEMM stays on the in-LDS-dequant kernel
+        (void)hipGetLastError();
+        img = nullptr;
+      } else {
+        m->w16[W] = img;
+        m->w16_bytes += bytes;
+        RC(launch_w4_expand_f16(w4_view(W, M, K), img, m->stream));
+        ++nk;
+      }
     }
+  }
+  if (x16 && N >= G2_MIN_N && K % 64 == 0 && m->w16.count(W)) {
+    void *img = m->w16[W];
     const bool gelu = gq && gq_bias && M % QK == 0;
     const long ev = prof_begin(m);
     RC(launch_gemm_f16_256(img, M, K, x16, N, gelu ? gq_bias : bias, y, m->stream, gelu ? gq : nullptr));
