@@ -418,22 +418,38 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     }
     return;
   }
+#ifdef VSIM_G2_NOSTORE  // (timing-only A/B build: no output)
+  if (M > 0) return;
+#endif
+  // The f32 tile leaves through LDS: a lane's accumulator holds 4 consecutive rows m of one
+  // column n, so direct stores write 16 columns x 64 bytes per instruction; each wave instead
+  // writes its (BM/2) x 64 region into its own LDS area, CP columns at a time, and stores
+  // whole runs of (BM/2) floats per column (8-13 % of the GEMM's time, tools/gemm_ab.sh).
+  constexpr int MW = BM / 2, LDW = MW + 4;  // region rows; LDS row stride (floats, padded)
+  constexpr int CP = 8 * 32 * LDW * 4 <= 2 * NPC * G2_PIECE * 2 ? 32 : 16;  // columns per pass
+  __syncthreads();                           // (every wave is past its last LDS operand read)
+  float *ep = (float *)g2lds + wave * CP * LDW;
+  const bool vec = (M & 3) == 0;
 #pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    const int m = mw + i * 16 + 4 * fk;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (bias) {
+  for (int pass = 0; pass < 64 / CP; ++pass) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = m + e < M ? bias[m + e] : 0.0f;
-    }
+    for (int i = 0; i < MR; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + fr;
-      if (n >= N) continue;
-      const float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+      for (int jj = 0; jj < CP / 16; ++jj)
+        *(f32x4 *)(ep + (16 * jj + fr) * LDW + 16 * i + 4 * fk) = acc[i][(CP / 16) * pass + jj];
+    // (a wave's own LDS writes and reads are ordered)
+    for (int idx = lane; idx < CP * (MW / 4); idx += 64) {
+      const int nl = idx / (MW / 4), c = idx % (MW / 4);
+      const int n = n0 + wc * 64 + CP * pass + nl, m = mw + 4 * c;
+      f32x4 v = *(const f32x4 *)(ep + nl * LDW + 4 * c);
+      if (n >= N || m >= M) continue;
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += m + e < M ? bias[m + e] : 0.0f;
+      }
       float *dst = Y + (size_t)n * M + m;
-      if ((M & 3) == 0 && m + 3 < M) {
-        *(float4 *)dst = make_float4(v[0], v[1], v[2], v[3]);
+      if (vec && m + 3 < M) {
+        *(f32x4 *)dst = v;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
