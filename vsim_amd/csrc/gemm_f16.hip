@@ -378,7 +378,15 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
   // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
   const int mw = m0 + wr * (BM / 2);  // the wave's first row
+  constexpr int MW = BM / 2;  // the wave's region: MW rows x 64 columns
   if constexpr (GQ) {
+    // quantized fp16 values go through LDS too (as the f32 tile below): direct stores would
+    // write 32-byte pieces of 16 columns per instruction
+    constexpr int LDH = MW + 8;  // LDS row stride (halves, padded)
+    __syncthreads();
+    _Float16 *eh = g2lds + wave * 32 * LDH;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int p = 0; p < AP; ++p) {
       const int mb = mw + 32 * p;  // the block's first row
@@ -389,7 +397,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
         bv[4 + e] = mb + 16 + 4 * fk + e < M ? bias[mb + 16 + 4 * fk + e] : 0.0f;
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 2 * pass; j < 2 * pass + 2; ++j) {
         float v[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -408,13 +416,18 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
         _Float16 h[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) h[e] = (_Float16)(d * (float)(x86_round_i8(v[e] * id)));
-        const int n = n0 + wc * 64 + j * 16 + fr;
-        if (n < N && mb < M) {
-          _Float16 *dst = Q16 + (size_t)n * M + mb + 4 * fk;
-          *(uint2 *)dst = *(const uint2 *)&h[0];
-          *(uint2 *)(dst + 16) = *(const uint2 *)&h[4];
-        }
+        _Float16 *row = eh + ((j & 1) * 16 + fr) * LDH + 32 * p + 4 * fk;
+        *(uint2 *)row = *(const uint2 *)&h[0];
+        *(uint2 *)(row + 16) = *(const uint2 *)&h[4];
       }
+    }
+    // (M % 32 == 0: a chunk of 8 rows is wholly in or out)
+    for (int idx = lane; idx < 32 * (MW / 8); idx += 64) {
+      const int nl = idx / (MW / 8), c = idx % (MW / 8);
+      const int n = n0 + wc * 64 + 32 * pass + nl, m = mw + 8 * c;
+      const uint4 v = *(const uint4 *)(eh + nl * LDH + 8 * c);
+      if (n < N && m < M) *(uint4 *)(Q16 + (size_t)n * M + m) = v;
+    }
     }
     return;
   }
@@ -425,7 +438,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   // column n, so direct stores write 16 columns x 64 bytes per instruction; each wave instead
   // writes its (BM/2) x 64 region into its own LDS area, CP columns at a time, and stores
   // whole runs of (BM/2) floats per column (8-13 % of the GEMM's time, tools/gemm_ab.sh).
-  constexpr int MW = BM / 2, LDW = MW + 4;  // region rows; LDS row stride (floats, padded)
+  constexpr int LDW = MW + 4;  // LDS row stride (floats, padded)
   constexpr int CP = 8 * 32 * LDW * 4 <= 2 * NPC * G2_PIECE * 2 ? 32 : 16;  // columns per pass
   __syncthreads();                           // (every wave is past its last LDS operand read)
   float *ep = (float *)g2lds + wave * CP * LDW;
