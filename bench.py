@@ -2,9 +2,9 @@
 """Headline benchmark: GPT-J-6B Q4_0 decode tokens/s on MI355X (BASELINE.json configs[1]).
 
 A step = one decode eval of one token through the device-resident executor of
-libvsim_hip.so (28 layers + lm_head, vsim.cpp:470-747 op sequence composed for GPT-J),
-plus the logits row back to the host and a greedy pick — the reference's decode loop
-(vsim.cpp:802-891).  Synthetic random-init weights of the GPT-J-6B shapes are drawn on
+libvsim_hip.so (28 layers + lm_head, vsim.cpp:470-747 op sequence composed for GPT-J) and
+the greedy pick on the device, fed to the next step (vsim_model_generate) — the reference's
+decode loop (vsim.cpp:802-891) without a host round trip per token.  Synthetic random-init weights of the GPT-J-6B shapes are drawn on
 the device (no checkpoints offline).  Decode starts after a 5-token prompt
 (50278 12092 2 0 50281, the reference's own run prompt), so step k attends over 5+k
 cached positions.
@@ -12,7 +12,9 @@ cached positions.
 N > 1 GPUs: GPT-J-6B is below the >=12B threshold at which the north star splits layers,
 so each rank decodes its own stream (replicas, weak scaling, no collective on the data
 path); value = all ranks' tokens / max-over-ranks time.  `--config gpt-neoxt-20b
---pipeline` runs the 20B layer split with one RCCL send of the residual per stage.
+--pipeline` runs the 20B layer split with one RCCL send of the residual per stage; the
+default run also measures that split over the same N ranks in a child job and reports it
+beside the headline as `pipeline_20b` (north star: 1/2/4/8-GPU numbers for the 20B).
 
 Prints ONE JSON line (rank 0) with `roofline` (the Q4_0 GEMV kernel: algorithmic weight
 bytes / event-timed average launch) and `cpu_baseline` (the CPU oracle on the host cores,
@@ -332,6 +334,39 @@ def run_pipeline(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def pipeline_companion(args, world, rank, local, steps=64, warmup=8, limit=300):
+    """GPT-NeoXT-20B split over the same `world` ranks (run_pipeline), run as a child job of
+    each rank on its own rendezvous port, so that a failure or a hang there (bounded by
+    `limit`, then the child is killed) cannot take the headline measurement with it.  Rank 0
+    returns the child's line, or the reason it has none."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    if world > 1:  # a store of its own: rank 0 of the child job hosts it
+        env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=str(int(os.environ.get("MASTER_PORT", "29500")) + 17))
+    else:
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            env.pop(k, None)
+    cmd = [sys.executable, os.path.abspath(__file__), "--pipeline", "--config", "gpt-neoxt-20b",
+           "--steps", str(steps), "--warmup", str(warmup), "--mode", args.mode,
+           "--dist-backend", args.dist_backend]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=limit)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {limit} s"}
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    if rank != 0:
+        return None
+    js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not js:
+        return {"error": "no JSON line", "stdout_tail": r.stdout[-400:]}
+    d = json.loads(js[-1])
+    return {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
+            "scaling": d["scaling"], "steps": d["steps"], "config": d["config"]}
+
+
 def run_prefill(args, dev):
     """One prompt eval of args.prefill tokens (codegen-16B, N = 2048) in
     fast mode: every Q4_0 matmul on fp16 MFMA (gemm_f16.hip: for N >= 256 the 256 x 256-tile
@@ -398,6 +433,8 @@ def main():
                     help="time one prompt eval of this many tokens instead of decode (fast-mode fp16 MFMA GEMM)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: host-staged sends, for rehearsing the pipeline with ranks sharing a GPU")
+    ap.add_argument("--no-pipeline-20b", action="store_true",
+                    help="skip the GPT-NeoXT-20B layer-split companion measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -426,7 +463,7 @@ def main():
     model = hip.Model.create(arch, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
                                         n_layer=hp.n_layer, n_rot=hp.n_rot,
                                         use_parallel_residual=hp.use_parallel_residual),
-                             n_ctx=n_ctx, device=local)
+                             n_ctx=n_ctx, device=dev)
     model.randomize(seed=1234 + rank, std=0.02)
     model.set_mode(hip.MODE_EXACT if args.mode == "exact" else hip.MODE_FAST)
     model.set_graph(not args.no_graph)
@@ -459,7 +496,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -509,6 +546,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(arch_s, hp)
     model.close()
+    if not args.no_pipeline_20b and args.config == "gpt-j-6B":
+        if dist is not None:
+            dist.barrier()
+        line["pipeline_20b"] = pipeline_companion(args, world, rank, local)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

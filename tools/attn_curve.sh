@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof_notail
 VSIM_TAIL=0 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_notail -o run --output-format csv -- \
-  python3 bench.py --steps 248 --warmup 8 --no-cpu-baseline --no-fast --no-profile > gpurun_out/notail.log 2>&1 || exit $?
+  python3 bench.py --steps 248 --warmup 8 --no-cpu-baseline --no-pipeline-20b --no-fast --no-profile > gpurun_out/notail.log 2>&1 || exit $?
 python3 - <<'PY'
 import csv, glob
 f = glob.glob('gpurun_out/prof_notail/**/run_kernel_trace.csv', recursive=True)

@@ -24,7 +24,7 @@ tail -3 gpurun_out/bench.log
 if [ "${PROF:-1}" = "1" ]; then
   export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-    python3 bench.py --steps 32 --warmup 4 --no-cpu-baseline --no-profile ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+    python3 bench.py --steps 32 --warmup 4 --no-cpu-baseline --no-pipeline-20b --no-profile ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
   stop_if_fatal $? rocprof
   find gpurun_out/prof -name "*stats*" | head
 fi

@@ -8,12 +8,12 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   > gpurun_out/fast_tests.log 2>&1
 rc=$?; echo "[gpu_fast] tests exit=$rc"; grep -E "passed|failed|^(tiny|small)|\[\(" gpurun_out/fast_tests.log | tail -12
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --mode fast --steps 64 --warmup 4 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_fast.log 2>&1
+timeout -k 10 300 python bench.py --mode fast --steps 64 --warmup 4 --no-cpu-baseline --no-pipeline-20b ${BENCH_ARGS:-} > gpurun_out/bench_fast.log 2>&1
 rc=$?; echo "[gpu_fast] bench exit=$rc"; tail -1 gpurun_out/bench_fast.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fast -o run --output-format csv -- \
-  python3 bench.py --mode fast --steps 32 --warmup 4 --no-cpu-baseline --no-profile ${BENCH_ARGS:-} > gpurun_out/prof_fast.log 2>&1
+  python3 bench.py --mode fast --steps 32 --warmup 4 --no-cpu-baseline --no-pipeline-20b --no-profile ${BENCH_ARGS:-} > gpurun_out/prof_fast.log 2>&1
 rc=$?; echo "[gpu_fast] rocprof exit=$rc"
 python3 - <<'PY'
 import csv, glob
