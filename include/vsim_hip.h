@@ -135,6 +135,16 @@ int vsim_op_gemm_f16(const void *w16, int M, int K, const void *x16, int n, cons
 int vsim_op_act_quant_f16(const float *x, int K, int n, const float *bias, int gelu, void *x16, void *stream);
 int vsim_op_gemm_f16_gelu_q(const void *w16, int M, int K, const void *x16, int n, const float *bias, void *q16,
                             void *stream);
+/* The same GEMM with the prompt layer's next step in its f32 epilogue:
+ *  _rope: GPT-J rotary pairs (rows m, m+1 with m % d < n_rot, even m) at position p0 + n, as
+ *    the rope + KV-write step of vsim.cpp:553-580 computes them (double cos/sin table cs
+ *    [pos][n_rot/2][2], the products and differences in double, rounded to float);
+ *  _join: the residual, res = res + (res_a + y) (vsim.cpp:694-695), or y + res when res_a is
+ *    NULL (vsim.cpp:657), in place.  M % 4 == 0. */
+int vsim_op_gemm_f16_rope(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                          const double *cs, int d, int n_rot, int p0, void *stream);
+int vsim_op_gemm_f16_join(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *res,
+                          const float *res_a, void *stream);
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream);
 /* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);

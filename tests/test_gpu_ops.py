@@ -288,6 +288,52 @@ def test_prefill_gemm_f16_256(M, K, N):
     assert not bad.any(), f"{bad.sum()} of {bad.size} outside the bound, first {np.argwhere(bad)[:4].tolist()}"
 
 
+@pytest.mark.parametrize("M,K,N,d,n_rot,p0", [(512, 256, 300, 128, 64, 0), (1024, 128, 257, 256, 64, 37),
+                                              (6144, 512, 520, 256, 64, 5)])
+def test_prefill_gemm_rope_join_epilogues_bit_identical(M, K, N, d, n_rot, p0):
+    """The long-prompt GEMM with RoPE (Q and K of a GPT-J prompt, written straight to their
+    cache rows) or the residual join (fc_out) in its epilogue: bit-identical to the plain GEMM
+    followed by the step's own arithmetic -- k_rope_kv_write's double products rounded to
+    float (vsim.cpp:553-580), k_add_residual's inpL + (attn + ff) and ff + inpL orders
+    (vsim.cpp:694-695, 657) -- restated here in numpy (ragged N, n_past > 0)."""
+    rng = np.random.default_rng(M + K + N + p0)
+    W16 = (rng.standard_normal((M, K)) * 0.05).astype(np.float16)
+    X16 = (rng.standard_normal((N, K)) * 0.5).astype(np.float16)
+    b = (rng.standard_normal(M) * 0.1).astype(np.float32)
+    w, x, bd = torch.from_numpy(W16).to(DEV), torch.from_numpy(X16).to(DEV), dev(b)
+    L = hip.lib()
+    y = torch.empty(N * M, dtype=torch.float32, device=DEV)
+    hip.check(L.vsim_op_gemm_f16(w.data_ptr(), M, K, x.data_ptr(), N, bd.data_ptr(), y.data_ptr(), None), "gemm")
+    y0 = y.cpu().numpy().reshape(N, M)
+    # RoPE: the table as the model builds it ([pos][n_rot/2] of (cos, sin) in double)
+    half = n_rot // 2
+    pos = np.arange(p0 + N, dtype=np.float64)[:, None]
+    theta = pos * 10000.0 ** (-2.0 * np.arange(half, dtype=np.float64) / n_rot)[None, :]
+    cs = np.stack([np.cos(theta), np.sin(theta)], axis=-1)  # [pos][half][2]
+    yr = torch.empty(N * M, dtype=torch.float32, device=DEV)
+    csd = torch.from_numpy(np.ascontiguousarray(cs)).to(DEV)
+    hip.check(L.vsim_op_gemm_f16_rope(w.data_ptr(), M, K, x.data_ptr(), N, bd.data_ptr(), yr.data_ptr(),
+                                      csd.data_ptr(), d, n_rot, p0, None), "rope")
+    ref = y0.copy()
+    hd = ref.reshape(N, M // d, d)
+    x0, x1 = hd[:, :, 0:n_rot:2].astype(np.float64), hd[:, :, 1:n_rot:2].astype(np.float64)
+    c = cs[p0:p0 + N, :, 0][:, None, :]
+    s = cs[p0:p0 + N, :, 1][:, None, :]
+    r0, r1 = (x0 * c - x1 * s).astype(np.float32), (x0 * s + x1 * c).astype(np.float32)
+    hd[:, :, 0:n_rot:2], hd[:, :, 1:n_rot:2] = r0, r1
+    assert np.array_equal(yr.cpu().numpy().reshape(N, M).view(np.uint32), ref.view(np.uint32))
+    # residual join, parallel (res + (res_a + y)) and serial (y + res) orders, in place
+    R = rng.standard_normal((N, M)).astype(np.float32)
+    A = rng.standard_normal((N, M)).astype(np.float32)
+    for a in (A, None):
+        res = torch.from_numpy(R.copy()).to(DEV)
+        ad = torch.from_numpy(a).to(DEV) if a is not None else None
+        hip.check(L.vsim_op_gemm_f16_join(w.data_ptr(), M, K, x.data_ptr(), N, bd.data_ptr(), res.data_ptr(),
+                                          ad.data_ptr() if ad is not None else None, None), "join")
+        want = R + (a + y0) if a is not None else y0 + R
+        assert np.array_equal(res.cpu().numpy().view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
 @pytest.mark.parametrize("M,K,N", [(512, 256, 300), (1056, 128, 257), (4096, 1024, 512)])
 def test_prefill_gemm_gelu_epilogue_bit_identical(M, K, N):
     """fc_in of a long prompt with bias + GELU + Q4_0 quantize in the GEMM epilogue gives the

@@ -67,6 +67,24 @@ int vsim_op_gemm_f16_gelu_q(const void *w16, int M, int K, const void *x16, int 
   if (!w16 || !x16 || !q16) { set_error("gemm_f16_gelu_q: null argument"); return VSIM_EINVAL; }
   return launch_gemm_f16_256(w16, M, K, x16, n, bias, nullptr, (hipStream_t)stream, q16);
 }
+int vsim_op_gemm_f16_rope(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *y,
+                          const double *cs, int d, int n_rot, int p0, void *stream) {
+  if (!w16 || !x16 || !y || !cs || p0 < 0) { set_error("gemm_f16_rope: bad argument"); return VSIM_EINVAL; }
+  G2Epi e;
+  e.cs = (const double2 *)cs;
+  e.d = d;
+  e.n_rot = n_rot;
+  e.p0 = p0;
+  return launch_gemm_f16_256(w16, M, K, x16, n, bias, y, (hipStream_t)stream, nullptr, &e);
+}
+int vsim_op_gemm_f16_join(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *res,
+                          const float *res_a, void *stream) {
+  if (!w16 || !x16 || !res) { set_error("gemm_f16_join: null argument"); return VSIM_EINVAL; }
+  G2Epi e;
+  e.res = res;
+  e.res_a = res_a;
+  return launch_gemm_f16_256(w16, M, K, x16, n, bias, res, (hipStream_t)stream, nullptr, &e);
+}
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream) {
   return launch_get_rows(w, K, V, rows, n, y, (hipStream_t)stream);
 }

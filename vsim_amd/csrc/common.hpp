@@ -267,8 +267,18 @@ constexpr int G2_MIN_N = VSIM_G2_MIN_N;
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
 // q16 non-null: y is not written; bias + GELU + Q4_0 quantize of the result into q16 ([n][M]
 // fp16 values d*(q-8), the next GEMM's operand, as launch_act_quant_f16(y, ..., gelu) makes)
+// Extra work of its f32 epilogue (v = product + bias, per output row m and column n):
+//  * cs != null: GPT-J RoPE of the row pairs (m, m+1) with m % d < n_rot, at position p0 + n
+//    (k_rope_kv_write's arithmetic, ops_attn.hip), so Q and K leave the GEMM rotated;
+//  * res != null: y = res + (res_a + v), or v + res without res_a (k_add_residual's orders;
+//    y may be res).
+struct G2Epi {
+  const double2 *cs = nullptr;
+  int d = 0, n_rot = 0, p0 = 0;
+  const float *res = nullptr, *res_a = nullptr;
+};
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
-                        hipStream_t s, void *q16 = nullptr);
+                        hipStream_t s, void *q16 = nullptr, const G2Epi *epi = nullptr);
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call)

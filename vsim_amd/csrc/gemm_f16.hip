@@ -249,12 +249,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // (ggml.c:4113-4152) + quantize_row_q4_0 per 32 consecutive rows m + the values d*(q-8) as
 // fp16 into Q16[n][m] -- what k_act_quant_f16 makes of Y + bias, without Y's round trip.  A
 // 32-row block of one column n sits in 4 lanes (fk = 0..3) x 8 registers of two accumulators.
-template <bool GQ, int AP>
+// EM: the f32 epilogue's extra work (G2Epi): 0 none, 1 RoPE, 2 residual join.
+template <bool GQ, int AP, int EM>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
                                                                  const _Float16 *__restrict__ B, int N,
                                                                  const float *__restrict__ bias, float *__restrict__ Y,
                                                                  const uint16_t *__restrict__ gelu_tab,
-                                                                 _Float16 *__restrict__ Q16) {
+                                                                 _Float16 *__restrict__ Q16, const G2Epi epi) {
   constexpr int BM = 64 * AP, MR = 2 * AP;  // tile rows; 16-row M-reps per wave
   constexpr int NPC = AP + 4;               // pieces per buffer
   extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
@@ -451,14 +452,59 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
       for (int jj = 0; jj < CP / 16; ++jj)
         *(f32x4 *)(ep + (16 * jj + fr) * LDW + 16 * i + 4 * fk) = acc[i][(CP / 16) * pass + jj];
     // (a wave's own LDS writes and reads are ordered)
-    for (int idx = lane; idx < CP * (MW / 4); idx += 64) {
-      const int nl = idx / (MW / 4), c = idx % (MW / 4);
+    constexpr int RW = MW / 4, NIT = CP * RW / 64;  // float4 chunks per column run; per lane
+    static_assert(CP * RW % 64 == 0, "whole chunks per lane");
+    // the epilogue's extra inputs, all loaded before the pass's first store (Y may be epi.res,
+    // and a load behind a store it may alias waits for it: one exposed latency per chunk)
+    [[maybe_unused]] f32x4 xr[EM == 2 ? NIT : 1], xa[EM == 2 ? NIT : 1];
+    [[maybe_unused]] double2 cq[EM == 1 ? NIT : 1][2];
+    if constexpr (EM != 0) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
+        const int n = n0 + wc * 64 + CP * pass + nl, m = mw + 4 * c;
+        if (n >= N || m >= M) continue;
+        if constexpr (EM == 2) {
+          xr[it] = *(const f32x4 *)(epi.res + (size_t)n * M + m);
+          if (epi.res_a) xa[it] = *(const f32x4 *)(epi.res_a + (size_t)n * M + m);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int dd = (m + 2 * q) % epi.d;
+            cq[it][q] = dd < epi.n_rot ? epi.cs[(size_t)(epi.p0 + n) * (epi.n_rot / 2) + dd / 2] : make_double2(1.0, 0.0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
       const int n = n0 + wc * 64 + CP * pass + nl, m = mw + 4 * c;
       f32x4 v = *(const f32x4 *)(ep + nl * LDW + 4 * c);
       if (n >= N || m >= M) continue;
       if (bias) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += m + e < M ? bias[m + e] : 0.0f;
+      }
+      if constexpr (EM == 1) {  // (the launcher guarantees M % 4 == 0 and an even d: pairs stay in the run)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if ((m + 2 * q) % epi.d < epi.n_rot) {
+            const double2 cs = cq[it][q];
+            const double x0 = v[2 * q], x1 = v[2 * q + 1];
+            v[2 * q] = (float)(x0 * cs.x - x1 * cs.y);
+            v[2 * q + 1] = (float)(x0 * cs.y + x1 * cs.x);
+          }
+        }
+      }
+      if constexpr (EM == 2) {
+        if (epi.res_a) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = xr[it][e] + (xa[it][e] + v[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] + xr[it][e];
+        }
       }
       float *dst = Y + (size_t)n * M + m;
       if (vec && m + 3 < M) {
@@ -495,30 +541,37 @@ static int g2_ap(int M, int n) {
 
 template <int AP>
 static int g2_launch(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
-                     hipStream_t s, const uint16_t *tab, void *q16) {
+                     hipStream_t s, const uint16_t *tab, void *q16, const G2Epi &epi) {
   static bool attr = false;
   if (!attr) {
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<false, AP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 g2_lds_bytes(AP)));
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_f16_256<true, AP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 g2_lds_bytes(AP)));
+    const void *fns[] = {(const void *)k_gemm_f16_256<false, AP, 0>, (const void *)k_gemm_f16_256<false, AP, 1>,
+                         (const void *)k_gemm_f16_256<false, AP, 2>, (const void *)k_gemm_f16_256<true, AP, 0>};
+    for (const void *f : fns)
+      VSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, g2_lds_bytes(AP)));
     attr = true;
   }
   const int nwg = ((M + 64 * AP - 1) / (64 * AP)) * ((n + G2_BN - 1) / G2_BN);
-  if (q16)
-    hipLaunchKernelGGL((k_gemm_f16_256<true, AP>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s,
-                       (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16);
-  else
-    hipLaunchKernelGGL((k_gemm_f16_256<false, AP>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s,
-                       (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, nullptr, nullptr);
+#define G2_GO(GQ, EM, TAB, Q)                                                                              \
+  hipLaunchKernelGGL((k_gemm_f16_256<GQ, AP, EM>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s,     \
+                     (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, TAB, (_Float16 *)Q, epi)
+  if (q16) G2_GO(true, 0, tab, q16);
+  else if (epi.cs) G2_GO(false, 1, nullptr, nullptr);
+  else if (epi.res) G2_GO(false, 2, nullptr, nullptr);
+  else G2_GO(false, 0, nullptr, nullptr);
+#undef G2_GO
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
 
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
-                        hipStream_t s, void *q16) {
+                        hipStream_t s, void *q16, const G2Epi *epi) {
   if (K % G2_BK || K <= 0 || M <= 0 || n <= 0 || (q16 && (M % QK || !bias))) {
     set_error("f16 gemm: K must be a positive multiple of 64 (and M of 32, with a bias, for the GELU epilogue)");
+    return VSIM_EINVAL;
+  }
+  const G2Epi e = epi ? *epi : G2Epi{};
+  if ((e.cs || e.res) && (q16 || M % 4 || (e.cs && (e.d <= 0 || e.d % 2 || e.n_rot % 2 || e.n_rot > e.d)))) {
+    set_error("f16 gemm: RoPE / residual epilogue needs M % 4 == 0, even d >= n_rot, no GELU epilogue");
     return VSIM_EINVAL;
   }
   const uint16_t *tab = nullptr;
@@ -527,8 +580,8 @@ int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, c
     if (int rc = tables_get(&t)) return rc;
     tab = t.gelu_f16;
   }
-  return g2_ap(M, n) == 3 ? g2_launch<3>(A16, M, K, x16, n, bias, y, s, tab, q16)
-                          : g2_launch<4>(A16, M, K, x16, n, bias, y, s, tab, q16);
+  return g2_ap(M, n) == 3 ? g2_launch<3>(A16, M, K, x16, n, bias, y, s, tab, q16, e)
+                          : g2_launch<4>(A16, M, K, x16, n, bias, y, s, tab, q16, e);
 }
 
 int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s) {

@@ -487,44 +487,46 @@ int prof_collect(vsim_model *m) {
 
 double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 
+// The fp16 image of a weight for the long-prompt GEMM, made on first use (false: no room for
+// it, and that weight's GEMMs stay on the in-LDS-dequant kernel).
+bool g2_image(vsim_model *m, const void *W, int M, int K, int &nk) {
+  if (m->w16.count(W)) return true;
+  const size_t bytes = (size_t)M * K * sizeof(uint16_t);
+  void *img = nullptr;
+  if (hipMalloc(&img, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  m->w16[W] = img;
+  m->w16_bytes += bytes;
+  if (launch_w4_expand_f16(w4_view(W, M, K), img, m->stream) != VSIM_OK) return false;
+  ++nk;
+  return true;
+}
+
 // Quantize an activation and run one GEMV in the model's mode.  x16 non-null (fast-mode
 // prompt batches): the activation is already the GEMM's fp16 operand (launch_act_quant_f16).
 // gq (fc_in of a long prompt): bias gq_bias + GELU + quantize of the product straight into the
-// next GEMM's fp16 operand gq, in the GEMM's epilogue; *fused tells the caller whether it ran.
+// next GEMM's fp16 operand gq, in the GEMM's epilogue; epi: RoPE or the residual join in the
+// epilogue (G2Epi); *fused tells the caller whether either ran.
 int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_t *xq, float *xd, bool quantize,
        const float *bias, float *y, int &nk, const void *x16 = nullptr, void *gq = nullptr,
-       const float *gq_bias = nullptr, bool *fused = nullptr) {
+       const float *gq_bias = nullptr, bool *fused = nullptr, const G2Epi *epi = nullptr) {
   if (fused) *fused = false;
   if (quantize && !x16) {
     RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
     ++nk;
   }
-  if (x16 && N >= G2_MIN_N && K % 64 == 0) {
-    // long prompt: the 256-wide-tile GEMM on the weight's fp16 image (made on first use)
-    auto it = m->w16.find(W);
-    void *img = it == m->w16.end() ? nullptr : it->second;
-    if (!img) {
-      const size_t bytes = (size_t)M * K * sizeof(uint16_t);
-      if (hipMalloc(&img, bytes) != hipSuccess) {
-        // no room for the image: this GEMM stays on the in-LDS-dequant kernel
-        (void)hipGetLastError();
-        img = nullptr;
-      } else {
-        m->w16[W] = img;
-        m->w16_bytes += bytes;
-        RC(launch_w4_expand_f16(w4_view(W, M, K), img, m->stream));
-        ++nk;
-      }
-    }
-  }
-  if (x16 && N >= G2_MIN_N && K % 64 == 0 && m->w16.count(W)) {
+  // long prompt: the 256-wide-tile GEMM on the weight's fp16 image
+  if (x16 && N >= G2_MIN_N && K % 64 == 0 && g2_image(m, W, M, K, nk)) {
     void *img = m->w16[W];
     const bool gelu = gq && gq_bias && M % QK == 0;
     const long ev = prof_begin(m);
-    RC(launch_gemm_f16_256(img, M, K, x16, N, gelu ? gq_bias : bias, y, m->stream, gelu ? gq : nullptr));
+    RC(launch_gemm_f16_256(img, M, K, x16, N, gelu ? gq_bias : bias, y, m->stream, gelu ? gq : nullptr,
+                           gelu ? nullptr : epi));
     prof_end(m, ev, "k_gemm_f16_256 (prompt)", (double)M * K / QK * QBYTES);
     ++nk;
-    if (fused) *fused = gelu;
+    if (fused) *fused = gelu || epi;
     return VSIM_OK;
   }
   const long ev = prof_begin(m);
@@ -618,14 +620,30 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
     return pf ? launch_norm_f16q(x, x16, E, N, w, b, s) : launch_norm(x, y, E, N, w, b, s);
   };
   RC(norm(m->inpL, m->cur1, L.ln1_w, L.ln1_b, X.a));
-  // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
-  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a));
-  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, m->Kb, nk, X.a));
-  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, m->Vb, nk, X.a));
-  // KV write + RoPE (vsim.cpp:553-580)
   const size_t loff = (size_t)(il - m->l0) * m->n_ctx * E;
   float *kc = m->kcache + loff, *vc = m->vcache + loff;
-  RC(launch_rope_kv_write(gptj ? 1 : 0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, m->hp.n_rot, m->rope_cs, s)); ++nk;
+  // long GPT-J prompt: RoPE and the KV-cache write (vsim.cpp:553-580) in the Q/K/V GEMMs'
+  // epilogues -- K and V straight into their cache rows -- instead of a pass of their own
+  const bool g2 = pf && N >= G2_MIN_N && E % 64 == 0;
+  const bool rope_epi = g2 && gptj && g2_image(m, L.wq, E, E, nk) && g2_image(m, L.wk, E, E, nk) &&
+                        g2_image(m, L.wv, E, E, nk);
+  G2Epi er;
+  er.cs = m->rope_cs;
+  er.d = d;
+  er.n_rot = m->hp.n_rot;
+  er.p0 = n_past;
+  float *kout = rope_epi ? kc + (size_t)n_past * E : m->Kb, *vout = rope_epi ? vc + (size_t)n_past * E : m->Vb;
+  // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
+  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a, nullptr, nullptr,
+        nullptr, rope_epi ? &er : nullptr));
+  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, kout, nk, X.a, nullptr, nullptr,
+        nullptr, rope_epi ? &er : nullptr));
+  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, vout, nk, X.a));
+  // KV write + RoPE (vsim.cpp:553-580)
+  if (!rope_epi) {
+    RC(launch_rope_kv_write(gptj ? 1 : 0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, m->hp.n_rot, m->rope_cs, s));
+    ++nk;
+  }
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
@@ -671,8 +689,23 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   } else {
     RC(launch_gelu(m->fch, m->fch, N * F, L.bfc, F, s)); ++nk;
   }
-  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, m->ff, nk, X.b));
-  RC(launch_add_residual(m->inpL, m->attn, m->ff, N * E, (!gptj && !m->hp.use_parallel_residual) ? 1 : 0, s)); ++nk;
+  // fc_out; a long prompt joins the residual in its epilogue (vsim.cpp:694-695 or 657)
+  const bool serial = !gptj && !m->hp.use_parallel_residual;
+  G2Epi ej;
+  ej.res = m->inpL;
+  ej.res_a = serial ? nullptr : m->attn;
+  const bool join_epi = g2 && g2_image(m, L.wproj, E, F, nk);
+  bool joined = false;
+  RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, join_epi ? m->inpL : m->ff, nk, X.b, nullptr,
+        nullptr, &joined, join_epi ? &ej : nullptr));
+  if (joined != join_epi) {
+    set_error("prompt layer: residual epilogue not taken");
+    return VSIM_EINVAL;
+  }
+  if (!joined) {
+    RC(launch_add_residual(m->inpL, m->attn, m->ff, N * E, serial ? 1 : 0, s));
+    ++nk;
+  }
   return VSIM_OK;
 }
 

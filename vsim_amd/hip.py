@@ -29,7 +29,8 @@ EXPORTS = [
     "vsim_dropin_stats", "vsim_dropin_reset", "vsim_norm_fallbacks",
     "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_act_repack", "vsim_op_act_unpack",
     "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_q4_expand_f16", "vsim_op_gemm_f16",
-    "vsim_op_act_quant_f16", "vsim_op_gemm_f16_gelu_q", "vsim_op_get_rows",
+    "vsim_op_act_quant_f16", "vsim_op_gemm_f16_gelu_q", "vsim_op_gemm_f16_rope", "vsim_op_gemm_f16_join",
+    "vsim_op_get_rows",
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
     "vsim_op_attn_prefill",
     "vsim_op_tables",
@@ -117,6 +118,8 @@ def lib():
     L.vsim_op_gemm_f16.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp]
     L.vsim_op_act_quant_f16.argtypes = [vp, ci, ci, vp, ci, vp, vp]
     L.vsim_op_gemm_f16_gelu_q.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp]
+    L.vsim_op_gemm_f16_rope.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp, ci, ci, ci, vp]
+    L.vsim_op_gemm_f16_join.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp, vp]
     L.vsim_op_norm.argtypes = [vp, vp, ci, ci, vp, vp, vp]
     L.vsim_op_gelu.argtypes = [vp, vp, ci, vp]
     L.vsim_op_attn_softmax.argtypes = [vp, ci, ci, ci, ci, cf, vp]
