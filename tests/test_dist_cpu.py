@@ -150,3 +150,47 @@ def test_decode_steps_match_single_rank(world):
         return toks
 
     assert stream(world) == stream(1) == _stream(1)
+
+
+def test_bench_pipeline_companion_env_and_failure(monkeypatch):
+    """bench.py's `pipeline_20b` companion: the child job gets a rendezvous of its own (no
+    TORCHELASTIC_* agent store, MASTER_PORT + 17, the parent's rank) and a child that fails
+    is reported as an error, never raised into the headline run."""
+    import argparse
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    seen = {}
+
+    class R:
+        returncode = 0
+        stdout = ('{"value": 1.5, "unit": "tokens/s", "n_gpus": 2, "ms_per_step": 666.7, "scaling": "strong", '
+                  '"steps": 4, "config": {"parallelism": "pipeline2"}}\n')
+        stderr = ""
+
+    def fake_run(cmd, env, **kw):
+        seen["cmd"], seen["env"], seen["kw"] = cmd, env, kw
+        return R()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.setenv("TORCHELASTIC_USE_AGENT_STORE", "True")
+    args = argparse.Namespace(mode="exact", dist_backend="nccl")
+    out = bench.pipeline_companion(args, world=2, rank=0, local=0)
+    assert out["value"] == 1.5 and out["n_gpus"] == 2
+    env = seen["env"]
+    assert not any(k.startswith("TORCHELASTIC_") for k in env)
+    assert env["MASTER_PORT"] == "29517" and env["RANK"] == "0" and env["WORLD_SIZE"] == "2"
+    assert "--pipeline" in seen["cmd"] and "gpt-neoxt-20b" in seen["cmd"] and seen["kw"]["timeout"] > 0
+    # rank 1 returns nothing; a failing or hanging child is an error entry
+    assert bench.pipeline_companion(args, world=2, rank=1, local=1) is None
+    R.returncode = 3
+    assert bench.pipeline_companion(args, world=2, rank=0, local=0)["error"] == "exit 3"
+
+    def hang(cmd, env, **kw):
+        raise subprocess.TimeoutExpired(cmd, kw["timeout"])
+
+    monkeypatch.setattr(subprocess, "run", hang)
+    assert "timed out" in bench.pipeline_companion(args, world=1, rank=0, local=0)["error"]
