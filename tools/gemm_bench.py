@@ -1,10 +1,11 @@
 """Long-prompt GEMM timing (k_gemm_f16_256 via vsim_op_gemm_f16) at the codegen-16B shapes
 (N = 2048): TFLOP/s per shape, HIP events over repeated launches."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vsim_amd import hip  # noqa: E402
 
 N = 2048
