@@ -317,22 +317,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
               __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][kk], bb[j][kk], acc[AP * mh + i][2 * nh + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-#ifndef VSIM_G2_STAGE_IN_MMA
-#define VSIM_G2_STAGE_IN_MMA 0
-#endif
 #define G2_SYNC_MMA(MH, NH, BB)                        \
   __builtin_amdgcn_sched_barrier(0);                   \
   __builtin_amdgcn_s_barrier();                        \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
-  mma(MH, NH, BB);                                     \
-  __builtin_amdgcn_sched_barrier(0);
-// (A/B build VSIM_G2_STAGE_IN_MMA=1: the phase's DMA issued after the LDS-read wait, beside
-// its MFMAs, instead of with the reads)
-#define G2_SYNC_MMA_S(MH, NH, BB, STAGE)               \
-  __builtin_amdgcn_sched_barrier(0);                   \
-  __builtin_amdgcn_s_barrier();                        \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
-  if (VSIM_G2_STAGE_IN_MMA) { _Pragma("unroll") STAGE } \
   mma(MH, NH, BB);                                     \
   __builtin_amdgcn_sched_barrier(0);
   // prologue: tile 0 whole, tile 1's B pieces in flight (as if staged in P4 of tile -1)
@@ -349,32 +337,25 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     const int cb = t & 1;
     rdA(cb, 0);
     rdB(b0, cb, 0);
-    if (!VSIM_G2_STAGE_IN_MMA) {
 #pragma unroll
-      for (int p = 0; p < AP / 2; ++p) stage(t + 1, p);
-    }
-    G2_SYNC_MMA_S(0, 0, b0, for (int p = 0; p < AP / 2; ++p) stage(t + 1, p);)
+    for (int p = 0; p < AP / 2; ++p) stage(t + 1, p);
+    G2_SYNC_MMA(0, 0, b0)
     __builtin_amdgcn_s_barrier();
     rdB(b1, cb, 1);
-    if (!VSIM_G2_STAGE_IN_MMA) {
 #pragma unroll
-      for (int p = AP / 2; p < AP; ++p) stage(t + 1, p);
-    }
-    G2_SYNC_MMA_S(0, 1, b1, for (int p = AP / 2; p < AP; ++p) stage(t + 1, p);)
+    for (int p = AP / 2; p < AP; ++p) stage(t + 1, p);
+    G2_SYNC_MMA(0, 1, b1)
     __builtin_amdgcn_s_barrier();
     rdA(cb, 1);
     G2_SYNC_MMA(1, 1, b1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B pieces) landed
     __builtin_amdgcn_s_barrier();
-    if (!VSIM_G2_STAGE_IN_MMA) {
 #pragma unroll
-      for (int p = AP; p < NPC; ++p) stage(t + 2, p);
-    }
-    G2_SYNC_MMA_S(1, 0, b0, for (int p = AP; p < NPC; ++p) stage(t + 2, p);)
+    for (int p = AP; p < NPC; ++p) stage(t + 2, p);
+    G2_SYNC_MMA(1, 0, b0)
     __builtin_amdgcn_s_barrier();
   }
 #undef G2_SYNC_MMA
-#undef G2_SYNC_MMA_S
   if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
   // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
@@ -432,13 +413,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     }
     return;
   }
-#ifdef VSIM_G2_NOSTORE  // (timing-only A/B build: no output)
-  if (M > 0) return;
-#endif
   // The f32 tile leaves through LDS: a lane's accumulator holds 4 consecutive rows m of one
   // column n, so direct stores write 16 columns x 64 bytes per instruction; each wave instead
   // writes its (BM/2) x 64 region into its own LDS area, CP columns at a time, and stores
-  // whole runs of (BM/2) floats per column (8-13 % of the GEMM's time, tools/gemm_ab.sh).
+  // whole runs of (BM/2) floats per column (the direct stores cost 8-10 % of the GEMM).
   constexpr int LDW = MW + 4;  // LDS row stride (floats, padded)
   constexpr int CP = 8 * 32 * LDW * 4 <= 2 * NPC * G2_PIECE * 2 ? 32 : 16;  // columns per pass
   __syncthreads();                           // (every wave is past its last LDS operand read)
