@@ -37,11 +37,11 @@ def child(out):
         m.randomize(seed=77, std=0.05)
         m.set_mode(hip.MODE_FAST)
         rng = np.random.default_rng(3)
-        a = [int(v) for v in rng.integers(0, hp.n_vocab, 288)]
+        a = [int(v) for v in rng.integers(0, hp.n_vocab, 290)]
         b = [int(v) for v in rng.integers(0, hp.n_vocab, 300)]
         l1 = m.eval(0, a)
-        l2 = m.eval(288, b)  # a second long prompt on top of the cache
-        l3 = m.eval(588, [int(np.argmax(l2))])
+        l2 = m.eval(290, b)  # a second long prompt on top of the cache (n_past not a multiple of 8)
+        l3 = m.eval(590, [int(np.argmax(l2))])
         res[name] = np.concatenate([l1, l2, l3]).astype(np.float32)
         m.close()
     np.savez(out, **res)

@@ -34,16 +34,18 @@ constexpr int AP_BQ = 128, AP_BK = 64, AP_THREADS = 256;
 // with zeros to ldt, a multiple of AP_BK), so the attention workgroups stage both operand
 // tiles with 16-byte loads and stores.  64 keys x 64 columns per workgroup; V goes through
 // an LDS tile for the transpose.
+// Keys [f0, f1) are skipped (already written by the K / V GEMM epilogues).
 __global__ void __launch_bounds__(256) k_kv_f16(const float *__restrict__ kc, const float *__restrict__ vc, int E,
                                                  int d, int nk, int ldt, _Float16 *__restrict__ k16,
-                                                 _Float16 *__restrict__ vt16) {
+                                                 _Float16 *__restrict__ vt16, int f0, int f1) {
   __shared__ float tv[64][65];
   const int key0 = blockIdx.x * 64, col0 = blockIdx.y * 64;
+  if (key0 >= f0 && key0 + 64 <= f1) return;  // (a block of fresh keys only)
   const int tid = threadIdx.x;
   for (int e = tid; e < 64 * 16; e += 256) {  // 64 keys x 16 float4 columns
     const int kk = e / 16, c4 = (e % 16) * 4, key = key0 + kk;
     float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-    if (key < nk) {
+    if (key < nk && (key < f0 || key >= f1)) {
       kv = *(const float4 *)(kc + (size_t)key * E + col0 + c4);
       vv = *(const float4 *)(vc + (size_t)key * E + col0 + c4);
       ahalf4 hk = {(_Float16)kv.x, (_Float16)kv.y, (_Float16)kv.z, (_Float16)kv.w};
@@ -59,7 +61,15 @@ __global__ void __launch_bounds__(256) k_kv_f16(const float *__restrict__ kc, co
     const int cc = e / 16, k4 = (e % 16) * 4;
     const int col = col0 + cc, h = col / d, dim = col % d;
     ahalf4 hv = {(_Float16)tv[k4][cc], (_Float16)tv[k4 + 1][cc], (_Float16)tv[k4 + 2][cc], (_Float16)tv[k4 + 3][cc]};
-    if (key0 + k4 < ldt) *(ahalf4 *)(vt16 + ((size_t)h * d + dim) * ldt + key0 + k4) = hv;
+    _Float16 *dst = vt16 + ((size_t)h * d + dim) * ldt + key0 + k4;
+    const int k = key0 + k4;
+    if (k + 4 <= f0 || k >= f1) {
+      if (k < ldt) *(ahalf4 *)dst = hv;
+    } else {  // (a group that straddles the fresh range)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((k + j < f0 || k + j >= f1) && k + j < ldt) dst[j] = hv[j];
+    }
   }
 }
 
@@ -294,8 +304,14 @@ size_t attn_prefill_lds() {
   return (size_t)(2 * AP_BK * (D + 8) + 2 * D * (AP_BK + 8)) * sizeof(_Float16);
 }
 
+int attn_prefill_ldt(int nk) { return (nk + AP_BK - 1) / AP_BK * AP_BK; }
+_Float16 *attn_prefill_k16(void *scratch, int E, int nk) { return (_Float16 *)scratch; }
+_Float16 *attn_prefill_vt16(void *scratch, int E, int nk) {
+  return (_Float16 *)scratch + (size_t)attn_prefill_ldt(nk) * E;
+}
+
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
-                            float scale, float *out, hipStream_t s, void *scratch, size_t scratch_bytes) {
+                            float scale, float *out, hipStream_t s, void *scratch, size_t scratch_bytes, bool fresh) {
   if (!attn_prefill_supported(d)) {
     set_error("attention prefill: head dim must be 64, 96, 128 or 256");
     return VSIM_EINVAL;
@@ -305,13 +321,19 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
     set_error("attention prefill: n_embd must be a multiple of 64");
     return VSIM_EINVAL;
   }
-  const int ldt = (nk + AP_BK - 1) / AP_BK * AP_BK;
+  const int ldt = attn_prefill_ldt(nk);
   const size_t need = attn_prefill_scratch(E, nk);
   _Float16 *buf = (_Float16 *)scratch;
   const bool own = !buf || scratch_bytes < need;
+  if (own && fresh) {
+    set_error("attention prefill: fresh keys need the caller's scratch");
+    return VSIM_EINVAL;
+  }
   if (own) VSIM_HIP(hipMallocAsync((void **)&buf, need, s));
-  _Float16 *k16 = buf, *vt16 = buf + (size_t)ldt * E;
-  hipLaunchKernelGGL(k_kv_f16, dim3(ldt / 64, E / 64), dim3(256), 0, s, kc, vc, E, d, nk, ldt, k16, vt16);
+  _Float16 *k16 = attn_prefill_k16(buf, E, nk), *vt16 = attn_prefill_vt16(buf, E, nk);
+  const int f0 = fresh ? n_past : 0, f1 = fresh ? nk : 0;  // keys already converted
+  if (!(fresh && n_past == 0 && nk == ldt))  // (else every key is fresh and there is no padding)
+    hipLaunchKernelGGL(k_kv_f16, dim3(ldt / 64, E / 64), dim3(256), 0, s, kc, vc, E, d, nk, ldt, k16, vt16, f0, f1);
   const float qscale = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
   const dim3 grid(((N + AP_BQ - 1) / AP_BQ) * H);
   static bool attr = false;

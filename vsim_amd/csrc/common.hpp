@@ -271,19 +271,29 @@ int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
 //  * cs != null: GPT-J RoPE of the row pairs (m, m+1) with m % d < n_rot, at position p0 + n
 //    (k_rope_kv_write's arithmetic, ops_attn.hip), so Q and K leave the GEMM rotated;
 //  * res != null: y = res + (res_a + v), or v + res without res_a (k_add_residual's orders;
-//    y may be res).
+//    y may be res);
+//  * h16 != null (with or without RoPE): the result also as fp16 for the prompt attention,
+//    row-major at h16[(p0 + n) * M + m] (its K copy), or with h16_t, transposed at
+//    h16[m * h16_ld + p0 + n] (its V^T copy) -- what k_kv_f16 makes of the cache rows.
 struct G2Epi {
   const double2 *cs = nullptr;
   int d = 0, n_rot = 0, p0 = 0;
   const float *res = nullptr, *res_a = nullptr;
+  _Float16 *h16 = nullptr;
+  int h16_ld = 0, h16_t = 0;
 };
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
                         hipStream_t s, void *q16 = nullptr, const G2Epi *epi = nullptr);
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
-// smaller: allocated stream-ordered per call)
+// smaller: allocated stream-ordered per call); fresh: the new keys [n_past, n_past + N) are
+// already there (written by the K and V GEMM epilogues, attn_prefill_k16/_vt16 give where)
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
-                            float scale, float *out, hipStream_t s, void *scratch = nullptr, size_t scratch_bytes = 0);
+                            float scale, float *out, hipStream_t s, void *scratch = nullptr, size_t scratch_bytes = 0,
+                            bool fresh = false);
+int attn_prefill_ldt(int nk);  // V^T row length (keys padded to the key tile)
+_Float16 *attn_prefill_k16(void *scratch, int E, int nk);
+_Float16 *attn_prefill_vt16(void *scratch, int E, int nk);
 size_t attn_prefill_scratch(int E, int nk);
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
                       hipStream_t s);

@@ -249,7 +249,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // (ggml.c:4113-4152) + quantize_row_q4_0 per 32 consecutive rows m + the values d*(q-8) as
 // fp16 into Q16[n][m] -- what k_act_quant_f16 makes of Y + bias, without Y's round trip.  A
 // 32-row block of one column n sits in 4 lanes (fk = 0..3) x 8 registers of two accumulators.
-// EM: the f32 epilogue's extra work (G2Epi): 0 none, 1 RoPE, 2 residual join.
+// EM: the f32 epilogue's extra work (G2Epi): 0 none, 1 RoPE (+ the fp16 row copy), 2 residual
+// join, 3 the fp16 transposed copy.
 template <bool GQ, int AP, int EM>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
                                                                  const _Float16 *__restrict__ B, int N,
@@ -474,6 +475,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
             v[2 * q + 1] = (float)(x0 * cs.y + x1 * cs.x);
           }
         }
+        if (epi.h16) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          *(h4 *)(epi.h16 + (size_t)(epi.p0 + n) * M + m) = (h4){(_Float16)v[0], (_Float16)v[1], (_Float16)v[2],
+                                                                 (_Float16)v[3]};
+        }
       }
       if constexpr (EM == 2) {
         if (epi.res_a) {
@@ -491,6 +497,30 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (m + e < M) dst[e] = v[e];
+      }
+    }
+    if constexpr (EM == 3) {
+      // the pass's columns again, read down the LDS region: runs of 8 columns of one row m,
+      // as fp16, into row m of the transposed copy (4 lanes cover a row's 32 columns)
+      constexpr int C8 = CP / 8, NT2 = MW * C8 / 64;
+      static_assert(MW * C8 % 64 == 0, "whole runs per lane");
+#pragma unroll
+      for (int it = 0; it < NT2; ++it) {
+        const int idx = lane + 64 * it, c8 = idx % C8, ml = idx / C8;
+        const int m = mw + ml, nb = n0 + wc * 64 + CP * pass + 8 * c8;
+        if (m >= M || nb >= N) continue;
+        const float bm = bias ? bias[m] : 0.0f;
+        half8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (_Float16)(ep[(8 * c8 + j) * LDW + ml] + bm);
+        _Float16 *dst = epi.h16 + (size_t)m * epi.h16_ld + epi.p0 + nb;
+        if (nb + 8 <= N && ((epi.p0 + nb) & 7) == 0) {
+          *(half8 *)dst = h;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (nb + j < N) dst[j] = h[j];
+        }
       }
     }
   }
@@ -523,7 +553,8 @@ static int g2_launch(const void *A16, int M, int K, const void *x16, int n, cons
   static bool attr = false;
   if (!attr) {
     const void *fns[] = {(const void *)k_gemm_f16_256<false, AP, 0>, (const void *)k_gemm_f16_256<false, AP, 1>,
-                         (const void *)k_gemm_f16_256<false, AP, 2>, (const void *)k_gemm_f16_256<true, AP, 0>};
+                         (const void *)k_gemm_f16_256<false, AP, 2>, (const void *)k_gemm_f16_256<false, AP, 3>,
+                         (const void *)k_gemm_f16_256<true, AP, 0>};
     for (const void *f : fns)
       VSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, g2_lds_bytes(AP)));
     attr = true;
@@ -535,6 +566,7 @@ static int g2_launch(const void *A16, int M, int K, const void *x16, int n, cons
   if (q16) G2_GO(true, 0, tab, q16);
   else if (epi.cs) G2_GO(false, 1, nullptr, nullptr);
   else if (epi.res) G2_GO(false, 2, nullptr, nullptr);
+  else if (epi.h16) G2_GO(false, 3, nullptr, nullptr);
   else G2_GO(false, 0, nullptr, nullptr);
 #undef G2_GO
   VSIM_HIP(hipGetLastError());
@@ -548,8 +580,12 @@ int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, c
     return VSIM_EINVAL;
   }
   const G2Epi e = epi ? *epi : G2Epi{};
-  if ((e.cs || e.res) && (q16 || M % 4 || (e.cs && (e.d <= 0 || e.d % 2 || e.n_rot % 2 || e.n_rot > e.d)))) {
-    set_error("f16 gemm: RoPE / residual epilogue needs M % 4 == 0, even d >= n_rot, no GELU epilogue");
+  if ((e.cs || e.res || e.h16) && (q16 || M % 4 || (e.cs && (e.d <= 0 || e.d % 2 || e.n_rot % 2 || e.n_rot > e.d)))) {
+    set_error("f16 gemm: RoPE / residual / copy epilogue needs M % 4 == 0, even d >= n_rot, no GELU epilogue");
+    return VSIM_EINVAL;
+  }
+  if (e.h16 && (e.res || (e.cs ? e.h16_t != 0 : (e.h16_t == 0 || e.h16_ld < e.p0 + n)))) {
+    set_error("f16 gemm: the fp16 copy is row-major with RoPE, transposed (h16_ld >= p0 + n) without");
     return VSIM_EINVAL;
   }
   const uint16_t *tab = nullptr;

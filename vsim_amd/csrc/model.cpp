@@ -633,12 +633,29 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   er.n_rot = m->hp.n_rot;
   er.p0 = n_past;
   float *kout = rope_epi ? kc + (size_t)n_past * E : m->Kb, *vout = rope_epi ? vc + (size_t)n_past * E : m->Vb;
+  // ... and the new keys' fp16 copies for the prompt attention (K rows, V^T columns), which
+  // then converts only the cached keys before them
+  const bool attn16 = m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d) && E % 64 == 0;
+  if (attn16 && !m->pf_scratch) {  // (prompt evals are never graph-captured: allocating here is safe)
+    m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
+    VSIM_HIP(hipMalloc(&m->pf_scratch, m->pf_bytes));
+  }
+  const bool kv16_epi = rope_epi && attn16;
+  G2Epi ek = er, ev;
+  if (kv16_epi) {
+    ek.h16 = attn_prefill_k16(m->pf_scratch, E, n_past + N);
+    ev.h16 = attn_prefill_vt16(m->pf_scratch, E, n_past + N);
+    ev.h16_t = 1;
+    ev.h16_ld = attn_prefill_ldt(n_past + N);
+    ev.p0 = n_past;
+  }
   // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
   RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a, nullptr, nullptr,
         nullptr, rope_epi ? &er : nullptr));
   RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, kout, nk, X.a, nullptr, nullptr,
-        nullptr, rope_epi ? &er : nullptr));
-  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, vout, nk, X.a));
+        nullptr, rope_epi ? &ek : nullptr));
+  RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, vout, nk, X.a, nullptr, nullptr,
+        nullptr, kv16_epi ? &ev : nullptr));
   // KV write + RoPE (vsim.cpp:553-580)
   if (!rope_epi) {
     RC(launch_rope_kv_write(gptj ? 1 : 0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, m->hp.n_rot, m->rope_cs, s));
@@ -647,13 +664,10 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
-  if (m->mode == VSIM_MODE_FAST && N >= 8 && attn_prefill_supported(d) && E % 64 == 0) {
+  if (attn16) {
     // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
-    if (!m->pf_scratch) {  // (prompt evals are never graph-captured: allocating here is safe)
-      m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
-      VSIM_HIP(hipMalloc(&m->pf_scratch, m->pf_bytes));
-    }
-    RC(launch_attn_prefill_f16(m->Qb, kc, vc, d, H, N, n_past, scale, m->attn_in, s, m->pf_scratch, m->pf_bytes));
+    RC(launch_attn_prefill_f16(m->Qb, kc, vc, d, H, N, n_past, scale, m->attn_in, s, m->pf_scratch, m->pf_bytes,
+                               kv16_epi));
     nk += 2;
   } else {
     RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
