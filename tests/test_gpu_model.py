@@ -171,6 +171,30 @@ def test_pipeline_stages_equal_single_stage(tmp_path):
         ids = [int(np.argmax(lf))]
 
 
+def test_stage_step_needs_fresh_begin_after_eval(tmp_path):
+    """vsim_model_stage_step trusts a host copy of n_past that only stage_begin sets: an eval,
+    eval_argmax or generate in between moves the device n_past, so the next stage_step is
+    refused (VSIM_EINVAL) until stage_begin runs again (no KV row written past n_ctx)."""
+    import torch
+    arch_s, hp = mg.CONFIGS["tiny-neox"]
+    path = str(tmp_path / "sg.bin")
+    mg.write_model(path, arch_s, hp, seed=2, std=0.05)
+    m = hip.Model.load(path, hip.ARCH_GPTNEOX, n_ctx=64)
+    tok = torch.zeros(1, dtype=torch.int32, device="cuda")
+    m.stage_bind(tok_in=tok.data_ptr(), tok_out=tok.data_ptr())
+    m.eval(0, [1, 2, 3])
+    m.stage_begin(3)
+    m.stage_step()
+    for intervene in (lambda: m.eval(4, [5]), lambda: m.eval_argmax(5, 6), lambda: m.generate(6, 7, 2)):
+        intervene()
+        with pytest.raises(hip.VsimError, match="stage_begin first"):
+            m.stage_step()
+        m.stage_begin(8)
+        m.stage_step()
+    m.sync()
+    m.close()
+
+
 @pytest.mark.parametrize("cfg", ["small-gptj", "small-neox", "small-bloom", "small-neox-serial"])
 def test_graph_replay_bit_exact_vs_oracle(cfg, tmp_path):
     """The decode step captured once in a hipGraph and replayed (n_past and the token read

@@ -121,6 +121,7 @@ struct vsim_model {
 
   int graph_mode = -1;
   int graph_kernels = 0;
+  int graph_kernels_kind[4] = {0, 0, 0, 0};  // per decode_graph kind: kernels in one replay
 
   // Per-kernel profiling (bench.py's live roofline): with profiling on, the decode step runs
   // eagerly and an event pair brackets every launch, tagged with the kernel's name and the
@@ -204,6 +205,7 @@ void free_scratch(vsim_model *m) {
   m->xqa = nullptr;
   m->xda = nullptr;
   m->npast_dev = m->npast_host = nullptr;
+  m->st_npast = -1;  // the device n_past went with npast_dev: stage_step needs a new stage_begin
   m->inpL = m->cur1 = m->cur2 = m->Qb = m->Kb = m->Vb = m->attn_in = m->attn = m->ff = m->fch = m->kq = m->logits =
       nullptr;
   m->xq1 = m->xq2 = m->xq3 = nullptr;
@@ -492,14 +494,24 @@ double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 bool g2_image(vsim_model *m, const void *W, int M, int K, int &nk) {
   if (m->w16.count(W)) return true;
   const size_t bytes = (size_t)M * K * sizeof(uint16_t);
+  // budget: images never take the device below W16_HEADROOM free bytes, so scratch growth,
+  // a second model or the caller's own buffers still find room
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + W16_HEADROOM) {
+    (void)hipGetLastError();
+    return false;
+  }
   void *img = nullptr;
   if (hipMalloc(&img, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
-  m->w16[W] = img;
+  if (launch_w4_expand_f16(w4_view(W, M, K), img, m->stream) != VSIM_OK) {
+    (void)hipFree(img);
+    return false;
+  }
+  m->w16[W] = img;  // only once the expand is queued: a failed launch leaves no stale entry
   m->w16_bytes += bytes;
-  if (launch_w4_expand_f16(w4_view(W, M, K), img, m->stream) != VSIM_OK) return false;
   ++nk;
   return true;
 }
@@ -1550,6 +1562,7 @@ int decode_graph(vsim_model *m, int kind) {
   VSIM_HIP(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
   gmode = m->mode;
   m->graph_kernels = gk;
+  m->graph_kernels_kind[kind] = gk;
   return VSIM_OK;
 }
 
@@ -1571,11 +1584,12 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
   m->tok_host[0] = token;
   m->npast_host[0] = n_past;
   m->prof_npast = n_past;
+  m->st_npast = -1;  // this step sets the device n_past: a stage step needs a new stage_begin
   hipStream_t s = m->stream;
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 1));
     VSIM_HIP(hipGraphLaunch(m->gexec_am, s));
-    m->kernels_last = m->graph_kernels;
+    m->kernels_last = m->graph_kernels_kind[1];
   } else {
     int nk = 0;
     RC(upload_step(m));
@@ -1605,16 +1619,19 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   m->tok_host[0] = token;
   m->npast_host[0] = n_past;
   m->prof_npast = n_past;
+  m->st_npast = -1;  // the loop advances the device n_past: a stage step needs a new stage_begin
   RC(upload_step(m));
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 2));
     for (int i = 0; i < n_steps; ++i) VSIM_HIP(hipGraphLaunch(m->gexec_gen, s));
+    m->kernels_last = m->graph_kernels_kind[2];  // kernels of one decode step (argmax included)
   } else {
     for (int i = 0; i < n_steps; ++i) {
       int nk = 0;
       m->prof_npast = n_past + i;
       RC(enqueue_decode(m, nk));
       RC(launch_argmax_gen(m->logits, m->hp.n_vocab, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s));
+      m->kernels_last = nk + 1;
     }
   }
   VSIM_HIP(hipMemcpyAsync(tokens_out, m->hist_dev + n_past, sizeof(int32_t) * n_steps, hipMemcpyDeviceToHost, s));
@@ -1625,7 +1642,9 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
 
 int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, const float *resid_in, float *resid_out,
                     float *logits) {
+  if (!m) { set_error("eval: null model"); return VSIM_EINVAL; }
   if (N <= 0 || n_past < 0 || n_past + N > m->n_ctx) { set_error("eval: n_past + N exceeds n_ctx"); return VSIM_EINVAL; }
+  m->st_npast = -1;  // an eval sets the device n_past: a stage step needs a new stage_begin
   VSIM_HIP(hipSetDevice(m->device));
   RC(ensure_scratch(m, N));
   const int E = m->hp.n_embd, V = m->hp.n_vocab;
@@ -1743,7 +1762,7 @@ int vsim_model_stage_step(vsim_model *m) {
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 3));
     VSIM_HIP(hipGraphLaunch(m->gexec_st, m->stream));
-    m->kernels_last = m->graph_kernels;
+    m->kernels_last = m->graph_kernels_kind[1];
   } else {
     int nk = 0;
     RC(enqueue_stage(m, nk));
