@@ -257,21 +257,9 @@ def run_pipeline(args, world, rank, dev, dist):
     tokt = torch.zeros(1, dtype=torch.int64, device="cpu" if host else "cuda")
     ext = torch.cuda.ExternalStream(model.stream())
 
-    def send(t, dst):
-        if host:  # gloo: host-staged, after the model's stream has produced the bytes
-            model.sync()
-            dist.send(t.cpu(), dst=dst)
-        else:     # RCCL, ordered on the model's stream (the current stream inside `ext`)
-            dist.send(t, dst=dst)
-
-    def recv(t, src):
-        if host:
-            c = torch.empty(t.shape, dtype=t.dtype)
-            dist.recv(c, src=src)
-            t.copy_(c)
-            torch.cuda.current_stream().synchronize()
-        else:
-            dist.recv(t, src=src)
+    # gloo: host-staged after the model's stream has produced the bytes; RCCL: ordered on the
+    # model's stream (the current stream inside `ext`)
+    send, recv = pipeline.make_transport(dist, host, sync=model.sync)
 
     def stage(n_past, ids, resid_in, resid_out):
         return model.eval(n_past, ids, resid_in=resid_in, resid_out=resid_out)

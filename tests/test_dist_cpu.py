@@ -95,10 +95,12 @@ def test_pipeline_matches_single_rank(world):
     assert _stream(world) == _stream(1)
 
 
-def _run_steps(rank, world, port, out):
+def _run_steps(rank, world, port, out, host_staged=False):
     """pipeline.decode_steps with a stand-in stage step over bound buffers (the device-resident
     protocol of vsim_model_stage_step: token word in on rank 0, residual rows between ranks,
-    argmax token word out on the last rank), after a pipeline_step prompt."""
+    argmax token word out on the last rank), after a pipeline_step prompt.  The hand-offs are
+    bench.py's own transport (pipeline.make_transport): host_staged=False is the RCCL branch's
+    call sequence (the tensor straight to dist.send / dist.recv), here over gloo on CPU tensors."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -106,8 +108,8 @@ def _run_steps(rank, world, port, out):
     l0, l1 = pipeline.layer_range(L, world, rank)
     kv = {}
     stage = _stage_fn(l0, l1, first, last, kv)
-    send = (lambda t, dst: dist.send(t, dst=dst)) if world > 1 else None
-    recv = (lambda t, src: dist.recv(t, src=src)) if world > 1 else None
+    syncs = []
+    send, recv = pipeline.make_transport(dist, host_staged, sync=lambda: syncs.append(1)) if world > 1 else (None, None)
     prompt = [1, 4, 2]
     resid = torch.zeros((len(prompt), E), dtype=torch.float32)
     tok = torch.zeros(1, dtype=torch.int64)
@@ -125,6 +127,8 @@ def _run_steps(rank, world, port, out):
 
     pipeline.decode_steps(rank, world, step, 6, send, recv, rin, rout, tok,
                           record=lambda i: toks.append(int(tok[0])))
+    if world > 1 and not last:  # a host-staged send waits for the producing stream first
+        assert bool(syncs) == host_staged
     if last:
         out.put(toks)
     if world > 1:
@@ -132,15 +136,16 @@ def _run_steps(rank, world, port, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_decode_steps_match_single_rank(world):
-    """The device-resident decode protocol gives the same stream as the per-eval one."""
+@pytest.mark.parametrize("world,host_staged", [(2, False), (3, False), (4, False), (2, True)])
+def test_decode_steps_match_single_rank(world, host_staged):
+    """The device-resident decode protocol gives the same stream as the per-eval one, with the
+    stream-ordered (RCCL-branch) and the host-staged transports; world 4 splits 7 layers 2,2,2,1."""
     ctx = mp.get_context("spawn")
 
     def stream(w):
         q = ctx.Queue()
         port = _free_port()
-        procs = [ctx.Process(target=_run_steps, args=(r, w, port, q)) for r in range(w)]
+        procs = [ctx.Process(target=_run_steps, args=(r, w, port, q, host_staged)) for r in range(w)]
         for p in procs:
             p.start()
         toks = q.get(timeout=120)

@@ -1,4 +1,4 @@
-"""The layer split of SURVEY.md §8(e) on the real HIP stages: 2 and 3 ranks (separate
+"""The layer split of SURVEY.md §8(e) on the real HIP stages: 2, 3 and 4 ranks (separate
 processes sharing this box's one GPU, gloo with host staging, tests/workers/pipeline_worker.py)
 run the prompt through pipeline.pipeline_step and then greedy decode through
 pipeline.decode_steps with the device-resident stage step (vsim_model_stage_step: hipGraph,
@@ -29,10 +29,11 @@ def free_port():
 
 
 @pytest.mark.parametrize("cfg,world,graph,n_layer", [("small-neox", 2, 1, None), ("small-neox", 3, 1, 5),
-                                                     ("small-gptj", 2, 1, None), ("small-neox", 2, 0, None)])
+                                                     ("small-neox", 4, 1, 7), ("small-gptj", 2, 1, None),
+                                                     ("small-neox", 2, 0, None)])
 def test_pipeline_ranks_equal_single_stage(cfg, world, graph, n_layer, tmp_path):
     arch_s, hp = mg.CONFIGS[cfg]
-    if n_layer:  # more layers than ranks, uneven split (ceil(5/3) = 2, 2, 1)
+    if n_layer:  # more layers than ranks, uneven splits (ceil(5/3) = 2, 2, 1; ceil(7/4) = 2, 2, 2, 1)
         hp = mg.HParams(hp.n_vocab, hp.n_embd, hp.n_head, n_layer, hp.n_rot, hp.use_parallel_residual)
     arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
     path = str(tmp_path / f"{cfg}.bin")

@@ -42,16 +42,12 @@ def main():
     first, last = rank == 0, rank == world - 1
     E = a.n_embd
 
-    def send(t, dst):
+    def sync():
         model.sync()
         torch.cuda.synchronize()
-        dist.send(t.cpu(), dst=dst)
 
-    def recv(t, src):
-        c = torch.empty(t.shape, dtype=t.dtype)
-        dist.recv(c, src=src)
-        t.copy_(c)
-        torch.cuda.synchronize()
+    # bench.py's host-staged transport (gloo: the ranks share one GPU)
+    send, recv = pipeline.make_transport(dist, True, sync=sync)
 
     prompt = [50278, 12092, 2, 0, 50281][:5]
     prompt = [p % 128 for p in prompt]

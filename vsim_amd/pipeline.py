@@ -31,6 +31,39 @@ def layer_range(n_layer: int, world: int, rank: int) -> tuple[int, int]:
     return l0, l1
 
 
+def make_transport(dist, host_staged: bool, sync: Callable | None = None):
+    """(send, recv) for the stage hand-offs.
+
+    host_staged (gloo between ranks that hold device tensors): sync() first (the producing
+    stream has finished the bytes), then the tensor goes through host memory.  Otherwise
+    (RCCL, bench.py --dist-backend nccl) the tensor itself is handed to dist.send / dist.recv
+    with no host synchronisation: ProcessGroupNCCL orders the transfer after the work queued
+    on the current stream and the current stream's later work after the transfer, so inside
+    `torch.cuda.stream(ExternalStream(model.stream()))` stage step -> send -> next step stay
+    stream-ordered.  The same calls on CPU tensors run over gloo (tests/test_dist_cpu.py)."""
+    import torch
+
+    def send(t, dst):
+        if host_staged:
+            if sync is not None:
+                sync()
+            dist.send(t.cpu(), dst=dst)
+        else:
+            dist.send(t, dst=dst)
+
+    def recv(t, src):
+        if host_staged:
+            c = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(c, src=src)
+            t.copy_(c)
+            if t.is_cuda:
+                torch.cuda.current_stream().synchronize()
+        else:
+            dist.recv(t, src=src)
+
+    return send, recv
+
+
 def pipeline_step(rank: int, world: int, n_past: int, ids: Sequence[int],
                   stage: Callable, send: Callable, recv: Callable, resid, tok) -> int:
     """One eval of `ids` through every stage; returns the greedy next token on every rank
