@@ -22,6 +22,9 @@
 #define VSIM_GGML_MAX_OPT 4
 #define VSIM_GGML_MAX_NODES 4096
 
+/* A translation unit that already has the reference's own ggml.h (which defines GGML_MAX_DIMS,
+ * ggml.h:202) takes the types from it; the layouts are the same. */
+#ifndef GGML_MAX_DIMS
 enum ggml_type {
   GGML_TYPE_Q4_0,
   GGML_TYPE_Q4_1,
@@ -84,6 +87,7 @@ struct ggml_cgraph {
 };
 
 struct ggml_context;
+#endif /* GGML_MAX_DIMS */
 
 enum ggml_task_type {
   GGML_TASK_INIT = 0,

@@ -104,6 +104,21 @@ void vsim_graph_stats(uint64_t *computes, uint64_t *nodes, uint64_t *h2d_bytes, 
  * (monitor.c:182-262, show_time_sep).  Returns the report's full length. */
 int vsim_graph_set_profile(int enable);
 int vsim_graph_profile_report(char *buf, size_t cap);
+/* Decode fast path of vsim_graph_compute.  A single-token eval of gptneox_eval
+ * (vsim.cpp:470-747, use_parallel_residual = 1) is recognised node by node (52 nodes per
+ * layer in ggml_build_forward_expand order, plus get_rows and the final norm + lm_head) and
+ * runs as the model executor's fused decode step -- 3 launches per layer, replayed as one
+ * hipGraph -- on the weights and KV cache the per-node path mirrored, with the KQV grouping of
+ * cgraph->n_threads.  Every other graph (prompt batches, the serial residual) runs per node.
+ * VSIM_GRAPH_FAST=0 turns the fast path off.
+ * vsim_graph_match checks a graph on the host only (no device needed): 0 and the recognised
+ * shape in `info`, or VSIM_EINVAL with the first mismatch in vsim_last_error(). */
+typedef struct {
+  int32_t n_layer, n_embd, n_head, n_rot, n_vocab, n_ctx, n_past, token;
+} vsim_graph_match_info;
+int vsim_graph_match(const struct ggml_cgraph *cgraph, vsim_graph_match_info *info);
+/* evals that took the fast path, and fast-path plans built (one per weight set / n_threads) */
+void vsim_graph_fast_stats(uint64_t *fast_evals, uint64_t *plans);
 /* drop-in statistics: calls, bytes moved host<->device, device weight-cache size */
 void vsim_dropin_stats(uint64_t *calls, uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *cached_bytes);
 void vsim_dropin_reset(void);

@@ -154,6 +154,11 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   // into two LDS buffers; the chains read the tile from LDS.  (The KV-cache row n_past,
   // written above by this workgroup, is read back after the barriers.)
   float y = 0.0f;  // (c <= ATT_THREADS: one output element per thread)
+  // --threads > 1: the pool gives thread t the keys [t*dc, t*dc + dc), each summed from 0 into
+  // its own work row, and FINALIZE adds the rows in thread order, empty ones as +0
+  const int nth = A.kqv_nth > 1 ? A.kqv_nth : 1, dc = (nk + nth - 1) / nth;
+  float tot = 0.0f;
+  bool run0 = true;
   {
     constexpr int PER = (ATT_VTF / 4 + ATT_THREADS - 1) / ATT_THREADS;  // float4 per thread per tile
     const int KT = ATT_VTF / c, nt = (nk + KT - 1) / KT, n4 = KT * c / 4;
@@ -182,7 +187,19 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
       }
       __syncthreads();
       if (t + 3 < nt) { ATT_TLOAD(rc, t + 3) }
-      if (tid < c) {  // the chain: LDS reads eight keys ahead of the dependent adds
+      if (tid < c && nth > 1) {  // the reference pool's key runs (--threads > 1)
+        const int kn = min(KT, nk - t * KT);
+        const float *pt = pr + t * KT;
+        for (int j = 0; j < kn; ++j) {
+          const int kg = t * KT + j;
+          if (kg > 0 && kg % dc == 0) {  // run boundary: FINALIZE's dst += partial, in run order
+            tot = run0 ? y : tot + y;
+            run0 = false;
+            y = 0.0f;
+          }
+          y = y + buf[j * c + tid] * pt[j];
+        }
+      } else if (tid < c) {  // the chain: LDS reads eight keys ahead of the dependent adds
         const int kn = min(KT, nk - t * KT);
         const float *pt = pr + t * KT;
         int j = 0;
@@ -199,9 +216,11 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
         for (; j < kn; ++j) y = y + buf[j * c + tid] * pt[j];
       }
     }
-#define ATT_STEP
-#undef ATT_STEP
 #undef ATT_TLOAD
+    if (nth > 1) {
+      if (!run0) y = tot + y;
+      if (nth > (nk + dc - 1) / dc) y = y + 0.0f;  // the trailing empty work rows
+    }
     if (tid < c && A.out) st_out<CO>(A.out + h * d + c0 + tid, y);
   }
   // quantize the part's outputs: wave w holds columns c0 + 64w .. +63, two 32-blocks

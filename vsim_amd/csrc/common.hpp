@@ -9,7 +9,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
 #include <string>
+
+#include "../../include/vsim_hip.h"
 
 namespace vsim {
 
@@ -100,6 +103,9 @@ struct AttnJob {
   int d, H, n_rot, style;  // style 0 = GPT-NeoX rotate-half, 1 = GPT-J pairs
   int n_ctx;               // cache rows (sizes the LDS score array, attn_lds_floats)
   int nsplit;              // workgroups per head (column parts of KQV, attn.hpp); 0/1 = one
+  int kqv_nth;             // KQV key grouping of the reference's pool (ggml.c:4535-4581, FINALIZE
+                           // 4469-4493): keys in kqv_nth runs of ceil(nk/nth), each chained from 0,
+                           // run sums added in order; 0/1 = one chain (--threads 1)
   float scale;
   const float *alibi;      // BLOOM: per-head ALiBi slopes (null: none); the single query row
                            // j = 0 gets (j + 1) * m_h added after the scale (ggml.c:6184-6244)
@@ -323,5 +329,11 @@ int launch_randn_f32(float *x, int n, uint64_t seed, float stddev, float mean, h
 // host-side: cos/sin table of the reference RoPE angles (ggml.c:6117-6120 / 5952-5955),
 // cs[p*(n_dims/2) + j] = {cos(p*theta_j), sin(p*theta_j)}, theta_j = 10000^(-2j/n_dims)
 void rope_table_host(double2 *cs, int n_pos, int n_dims);
+
+// model.cpp: a whole-model executor on borrowed device buffers (graph.cpp's fast path) and its
+// per-call attention settings
+int model_create_impl(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
+                      const std::map<std::string, void *> *borrow, float *kc, float *vc, vsim_model **out);
+int model_set_attn(vsim_model *m, int kqv_nth, float scale);
 
 }  // namespace vsim

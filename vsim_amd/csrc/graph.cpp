@@ -66,6 +66,17 @@ struct Exec {
   uint64_t computes = 0, nodes = 0, h2d = 0, d2h = 0;
   bool prof = false;
   OpProf op[GGML_OP_COUNT + 2];  // + Q4_0 mul_mat, F32 mul_mat split out of MUL_MAT
+  uint64_t ext_gen = 0;          // bumped whenever a mirror of an external tensor changes
+  // decode fast path: the model executor bound to the mirrors of one set of matched tensors
+  struct Fast {
+    vsim_model *m = nullptr;
+    std::vector<const void *> key;  // the matched weight / cache tensors the model is bound to
+    uint64_t gen = 0;
+    int nth = 0;
+    float scale = 0.0f;
+  } fast;
+  bool fast_off = false;
+  uint64_t fast_evals = 0, fast_plans = 0;
 } X;
 
 constexpr int PROF_MM_Q4 = GGML_OP_COUNT, PROF_MM_F32 = GGML_OP_COUNT + 1;
@@ -82,6 +93,11 @@ int grow(void **p, size_t *cap, size_t want) {
 }
 
 void print_profile_at_exit();
+void print_stats_at_exit() {
+  // stderr: the front-end reads stdout (cformers/interface.py parses the token stream)
+  fprintf(stderr, "vsim_graph_compute: %llu computes, %llu on the decode fast path, %llu fast-path plans\n",
+          (unsigned long long)X.computes, (unsigned long long)X.fast_evals, (unsigned long long)X.fast_plans);
+}
 
 int ensure_ready() {
   if (X.ready) return VSIM_OK;
@@ -98,6 +114,8 @@ int ensure_ready() {
   DevTables t;
   if (int rc = tables_get(&t)) return rc;
   X.prof = getenv("VSIM_GRAPH_PROFILE") && atoi(getenv("VSIM_GRAPH_PROFILE")) != 0;
+  X.fast_off = getenv("VSIM_GRAPH_FAST") && atoi(getenv("VSIM_GRAPH_FAST")) == 0;
+  if (getenv("VSIM_GRAPH_STATS") && atoi(getenv("VSIM_GRAPH_STATS")) != 0) atexit(print_stats_at_exit);
   // like the reference's show_time_sep at the end of a run (vsim.cpp:905-908)
   if (X.prof) atexit(print_profile_at_exit);
   X.ready = true;
@@ -139,6 +157,11 @@ const Ext *q4_of(const ggml_tensor *t) {
   return &it->second;
 }
 
+void drop_fast() {
+  if (X.fast.m) vsim_model_free(X.fast.m);
+  X.fast = Exec::Fast{};
+}
+
 int register_ext(const ggml_tensor *t) {
   const char *h = (const char *)t->data;
   const size_t bytes = span(t);
@@ -147,9 +170,11 @@ int register_ext(const ggml_tensor *t) {
     if (it->second.bytes == bytes && it->second.type == (int)t->type && it->second.ne0 == t->ne[0] &&
         it->second.ne1 == t->ne[1])
       return VSIM_OK;
+    drop_fast();  // the plan's model may point at the buffer freed here
     if (it->second.dev) (void)hipFree(it->second.dev);
     if (it->second.w4) (void)hipFree(it->second.w4);
     X.ext.erase(it);
+    ++X.ext_gen;
   }
   Ext e{bytes, nullptr, nullptr, (int)t->type, t->ne[0], t->ne[1]};
   if (t->type == GGML_TYPE_Q4_0) {
@@ -174,6 +199,7 @@ int register_ext(const ggml_tensor *t) {
   }
   X.h2d += bytes;
   X.ext[h] = e;
+  ++X.ext_gen;
   return VSIM_OK;
 }
 
@@ -380,6 +406,299 @@ int node(const ggml_tensor *n, int nth, bool dry) {
   }
 }
 
+// ------------------------------------------------------------------ decode fast path
+// gptneox_eval (vsim.cpp:470-747) for one token with use_parallel_residual = 1, in the node
+// order ggml_build_forward_expand gives it.  With N = 1 every ggml_repeat of a [E] vector onto
+// a [E, 1] row returns the vector itself (same shape), so the biases and LayerNorm factors are
+// direct operands.  get_rows; per layer 42 nodes
+//   +0..2   norm(inpL), mul(ln1_w, .), add(., ln1_b)                      -> cur
+//   +3..6   mul_mat(wk, cur), add(., bk); view(memory_k), cpy             (K row to the cache)
+//   +7..10  mul_mat(wv, cur), add(., bv); view(memory_v), cpy             (V row to the cache)
+//   +11..13 view(memory_v), reshape, permute                              -> V_trans
+//   +14..17 view(memory_k), reshape, gptneox_rope(mode 1), permute        -> K
+//   +18..22 mul_mat(wq, cur), add(., bq), cpy, gptneox_rope(mode 0), permute -> Q
+//   +23..26 mul_mat(K, Q), scale, diag_mask_inf, soft_max
+//   +27..29 mul_mat(V_trans, KQ_soft_max), permute, cpy                   -> merged heads
+//   +30..31 mul_mat(wo, .), add(bo, .)                                    -> attn
+//   +32..34 norm(inpL), mul(ln2_w, .), add(., ln2_b)                      -> inpFF
+//   +35..37 mul_mat(wfc, .), add(bfc, .), gelu
+//   +38..39 mul_mat(wproj, .), add(bproj, .)                              -> ff
+//   +40..41 add(attn, ff), add(inpL, .)                                   -> inpL
+// then norm, mul, add (ln_f) and mul_mat(lm_head) as the last node.
+constexpr int NEOX_LAYER_NODES = 42, NEOX_HEAD_NODES = 4;
+
+struct NeoxLayer {
+  const ggml_tensor *ln1_w, *ln1_b, *ln2_w, *ln2_b, *wq, *bq, *wk, *bk, *wv, *bv, *wo, *bo, *wfc, *bfc, *wproj,
+      *bproj;
+};
+struct NeoxMatch {
+  vsim_graph_match_info info{};
+  float scale = 0.0f;
+  const ggml_tensor *wte = nullptr, *lnf_w = nullptr, *lnf_b = nullptr, *lmh = nullptr, *memk = nullptr,
+                    *memv = nullptr;
+  std::vector<NeoxLayer> layers;
+};
+
+bool match_neox_decode(const ggml_cgraph *g, NeoxMatch &M, std::string &why) {
+  const int nn = g->n_nodes;
+  auto node = [&](int i) -> const ggml_tensor * { return i >= 0 && i < nn ? g->nodes[i] : nullptr; };
+  auto leaf = [](const ggml_tensor *t) { return t && t->op == GGML_OP_NONE && t->data; };
+  auto flat = [](const ggml_tensor *t) { return t->ne[2] == 1 && t->ne[3] == 1; };
+  auto is = [](const ggml_tensor *t, int op) { return t && t->op == op; };
+  int E = 0, V = 0, H = 0, d = 0, P = -1, n_rot = -1;
+  auto vec = [&](const ggml_tensor *t, int n) {
+    return leaf(t) && t->type == GGML_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1 && flat(t);
+  };
+  auto mat = [&](const ggml_tensor *t, int K, int R) {
+    return leaf(t) && t->type == GGML_TYPE_Q4_0 && t->ne[0] == K && t->ne[1] == R && flat(t);
+  };
+  auto row = [](const ggml_tensor *t, int n) { return t->type == GGML_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1; };
+#define REQ(c, msg)  \
+  do {               \
+    if (!(c)) {      \
+      why = msg;     \
+      return false;  \
+    }                \
+  } while (0)
+  // LayerNorm + affine at nodes i..i+2: norm(x), mul(w, .), add(., b)
+  auto ln = [&](int i, const ggml_tensor *x, const ggml_tensor *&w, const ggml_tensor *&b) {
+    const ggml_tensor *a = node(i), *m = node(i + 1), *s = node(i + 2);
+    if (!(is(a, GGML_OP_NORM) && a->src0 == x && row(a, E) && is(m, GGML_OP_MUL) && m->src1 == a && vec(m->src0, E) &&
+          is(s, GGML_OP_ADD) && s->src0 == m && vec(s->src1, E)))
+      return false;
+    w = m->src0;
+    b = s->src1;
+    return true;
+  };
+  // Q4_0 linear + bias at nodes i..i+1 (the bias add in either operand order)
+  auto lin = [&](int i, const ggml_tensor *x, int K, int R, const ggml_tensor *&W, const ggml_tensor *&b) {
+    const ggml_tensor *mm = node(i), *s = node(i + 1);
+    if (!(is(mm, GGML_OP_MUL_MAT) && mm->src1 == x && mat(mm->src0, K, R) && row(mm, R) && is(s, GGML_OP_ADD)))
+      return false;
+    const ggml_tensor *bias = s->src0 == mm ? s->src1 : s->src1 == mm ? s->src0 : nullptr;
+    if (!vec(bias, R)) return false;
+    W = mm->src0;
+    b = bias;
+    return true;
+  };
+  auto i32s = [](const ggml_tensor *t, int n) {
+    return t && t->op == GGML_OP_NONE && t->data && t->type == GGML_TYPE_I32 && t->ne[0] == n && t->ne[1] == 1;
+  };
+  auto both = [](const ggml_tensor *s, const ggml_tensor *a, const ggml_tensor *b) {
+    return (s->src0 == a && s->src1 == b) || (s->src0 == b && s->src1 == a);
+  };
+  auto cache_view = [&](const ggml_tensor *v, long n) {
+    return is(v, GGML_OP_VIEW) && leaf(v->src0) && v->src0->type == GGML_TYPE_F32 && v->src0->ne[1] == 1 &&
+           flat(v->src0) && v->ne[0] == n && v->ne[1] == 1;
+  };
+  const ggml_tensor *n0 = node(0);
+  REQ(is(n0, GGML_OP_GET_ROWS), "first node is not get_rows");
+  REQ(leaf(n0->src0) && n0->src0->type == GGML_TYPE_Q4_0 && flat(n0->src0) && i32s(n0->src1, 1),
+      "get_rows: not one token of a Q4_0 table");
+  M.wte = n0->src0;
+  E = M.wte->ne[0];
+  V = M.wte->ne[1];
+  const int F = 4 * E;
+  M.info.token = *(const int32_t *)n0->src1->data;
+  const ggml_tensor *inpL = n0;
+  std::vector<long> koff, kvoff;  // per layer: K-row view and K-range view offsets (floats)
+  int i = 1;
+  while (i + NEOX_HEAD_NODES < nn) {
+    NeoxLayer Y{};
+    REQ(ln(i, inpL, Y.ln1_w, Y.ln1_b), "layer: input LayerNorm");
+    const ggml_tensor *cur = node(i + 2);
+    REQ(lin(i + 3, cur, E, E, Y.wk, Y.bk), "layer: key projection");
+    const ggml_tensor *vk = node(i + 5), *ck = node(i + 6);
+    REQ(cache_view(vk, E) && is(ck, GGML_OP_CPY) && ck->src0 == node(i + 4) && ck->src1 == vk,
+        "layer: K row into memory_k");
+    REQ(lin(i + 7, cur, E, E, Y.wv, Y.bv), "layer: value projection");
+    const ggml_tensor *vv = node(i + 9), *cv = node(i + 10);
+    REQ(cache_view(vv, E) && is(cv, GGML_OP_CPY) && cv->src0 == node(i + 8) && cv->src1 == vv,
+        "layer: V row into memory_v");
+    if (!M.memk) {
+      M.memk = vk->src0;
+      M.memv = vv->src0;
+    }
+    REQ(vk->src0 == M.memk && vv->src0 == M.memv && M.memk != M.memv && M.memk->ne[0] == M.memv->ne[0],
+        "layer: one memory_k / memory_v");
+    const ggml_tensor *a = node(i + 11), *b = node(i + 12), *c = node(i + 13);
+    REQ(is(a, GGML_OP_VIEW) && a->src0 == M.memv && is(b, GGML_OP_RESHAPE) && b->src0 == a && is(c, GGML_OP_PERMUTE) &&
+            c->src0 == b && b->ne[0] * b->ne[1] == E && a->ne[0] == (long)E * b->ne[2],
+        "layer: V_trans view");
+    if (!d) {
+      d = b->ne[0];
+      H = b->ne[1];
+    }
+    REQ(b->ne[0] == d && b->ne[1] == H, "layer: head shape");
+    const int nk = b->ne[2];  // n_past + 1
+    const ggml_tensor *vt = c, *vtv = a;
+    a = node(i + 14), b = node(i + 15), c = node(i + 16);
+    const ggml_tensor *kp = node(i + 17);
+    REQ(is(a, GGML_OP_VIEW) && a->src0 == M.memk && a->ne[0] == (long)E * nk && is(b, GGML_OP_RESHAPE) && b->src0 == a &&
+            b->ne[0] == d && b->ne[1] == H && b->ne[2] == nk && is(c, GGML_OP_GPTNEOX_ROPE) && c->src0 == b &&
+            i32s(c->src1, 3) && is(kp, GGML_OP_PERMUTE) && kp->src0 == c,
+        "layer: K range view + rope");
+    const int32_t *kr = (const int32_t *)c->src1->data;
+    if (P < 0) {
+      P = kr[0];
+      n_rot = kr[1];
+    }
+    REQ(kr[0] == P && kr[1] == n_rot && kr[2] == 1 && nk == P + 1, "layer: K rope parameters");
+    koff.push_back(((const char *)vk->data - (const char *)M.memk->data) / 4);
+    kvoff.push_back(((const char *)a->data - (const char *)M.memk->data) / 4);
+    REQ(((const char *)vv->data - (const char *)M.memv->data) / 4 == koff.back() &&
+            ((const char *)vtv->data - (const char *)M.memv->data) / 4 == kvoff.back(),
+        "layer: K / V cache offsets differ");
+    REQ(lin(i + 18, cur, E, E, Y.wq, Y.bq), "layer: query projection");
+    a = node(i + 20), b = node(i + 21), c = node(i + 22);
+    REQ(is(a, GGML_OP_CPY) && a->src0 == node(i + 19) && leaf(a->src1) && a->src1->ne[0] == d && a->src1->ne[1] == H &&
+            a->src1->ne[2] == 1 && is(b, GGML_OP_GPTNEOX_ROPE) && b->src0 == a && i32s(b->src1, 3) &&
+            is(c, GGML_OP_PERMUTE) && c->src0 == b,
+        "layer: Q copy + rope");
+    const int32_t *qr = (const int32_t *)b->src1->data;
+    REQ(qr[0] == P && qr[1] == n_rot && qr[2] == 0, "layer: Q rope parameters");
+    const ggml_tensor *qp = c;
+    a = node(i + 23), b = node(i + 24), c = node(i + 25);
+    const ggml_tensor *sm = node(i + 26);
+    REQ(is(a, GGML_OP_MUL_MAT) && a->src0 == kp && a->src1 == qp && is(b, GGML_OP_SCALE) && b->src0 == a &&
+            leaf(b->src1) && b->src1->type == GGML_TYPE_F32 && b->src1->ne[0] == 1 && is(c, GGML_OP_DIAG_MASK_INF) &&
+            c->src0 == b && i32s(c->src1, 1) && *(const int32_t *)c->src1->data == P && is(sm, GGML_OP_SOFT_MAX) &&
+            sm->src0 == c,
+        "layer: KQ, scale, mask, soft_max");
+    const float sc = *(const float *)b->src1->data;
+    if (M.scale == 0.0f) M.scale = sc;
+    REQ(sc == M.scale && sc != 0.0f, "layer: attention scale");
+    a = node(i + 27), b = node(i + 28), c = node(i + 29);
+    REQ(is(a, GGML_OP_MUL_MAT) && a->src0 == vt && a->src1 == sm && is(b, GGML_OP_PERMUTE) && b->src0 == a &&
+            is(c, GGML_OP_CPY) && c->src0 == b && leaf(c->src1) && c->src1->ne[0] == E && c->src1->ne[1] == 1,
+        "layer: KQV and head merge");
+    REQ(lin(i + 30, c, E, E, Y.wo, Y.bo), "layer: output projection");
+    const ggml_tensor *attn = node(i + 31);
+    REQ(ln(i + 32, inpL, Y.ln2_w, Y.ln2_b), "layer: post-attention LayerNorm (parallel residual)");
+    REQ(lin(i + 35, node(i + 34), E, F, Y.wfc, Y.bfc), "layer: fc_in");
+    a = node(i + 37);
+    REQ(is(a, GGML_OP_GELU) && a->src0 == node(i + 36), "layer: gelu");
+    REQ(lin(i + 38, a, F, E, Y.wproj, Y.bproj), "layer: fc_out");
+    a = node(i + 40), b = node(i + 41);
+    REQ(is(a, GGML_OP_ADD) && both(a, attn, node(i + 39)) && is(b, GGML_OP_ADD) && both(b, inpL, a),
+        "layer: residual joins");
+    inpL = b;
+    M.layers.push_back(Y);
+    i += NEOX_LAYER_NODES;
+  }
+  const int L = (int)M.layers.size();
+  REQ(L > 0 && i + NEOX_HEAD_NODES == nn, "node count is not 1 + 42 * n_layer + 4");
+  REQ(ln(i, inpL, M.lnf_w, M.lnf_b), "final LayerNorm");
+  const ggml_tensor *lm = node(i + 3);
+  REQ(is(lm, GGML_OP_MUL_MAT) && lm->src1 == node(i + 2) && mat(lm->src0, E, V) && row(lm, V), "lm_head");
+  M.lmh = lm->src0;
+  // the cache: memory_k = [n_layer][n_ctx][E] floats (vsim.cpp:357-361), rows at (il*n_ctx + n_past)*E
+  const long total = M.memk->ne[0];
+  REQ(total % ((long)L * E) == 0, "memory_k size is not n_layer * n_ctx * n_embd");
+  const int n_ctx = (int)(total / ((long)L * E));
+  for (int il = 0; il < L; ++il)
+    REQ(koff[il] == ((long)il * n_ctx + P) * E && kvoff[il] == (long)il * n_ctx * E, "KV cache offsets of a layer");
+  REQ(P >= 0 && P + 1 <= n_ctx, "n_past outside the cache");
+  REQ(n_rot > 0 && n_rot <= d && n_rot % 2 == 0 && E % 128 == 0, "shape outside the fused step's range");
+  M.info.n_layer = L;
+  M.info.n_embd = E;
+  M.info.n_head = H;
+  M.info.n_rot = n_rot;
+  M.info.n_vocab = V;
+  M.info.n_ctx = n_ctx;
+  M.info.n_past = P;
+#undef REQ
+  return true;
+}
+
+// what a plan is bound to: every matched weight and the cache, the thread count, the scale
+std::vector<const void *> plan_key(const NeoxMatch &M) {
+  std::vector<const void *> k{M.wte, M.lmh, M.lnf_w, M.lnf_b, M.memk, M.memv};
+  for (const NeoxLayer &Y : M.layers)
+    for (const ggml_tensor *t : {Y.ln1_w, Y.ln1_b, Y.ln2_w, Y.ln2_b, Y.wq, Y.bq, Y.wk, Y.bk, Y.wv, Y.bv, Y.wo, Y.bo,
+                                 Y.wfc, Y.bfc, Y.wproj, Y.bproj})
+      k.push_back(t);
+  return k;
+}
+
+std::string layer_name(int il, const char *what) { return "gpt_neox.layers." + std::to_string(il) + "." + what; }
+
+// Build the fast-path model on the mirrors of a matched graph (its leafs are registered).
+int build_fast(const NeoxMatch &M, int nth) {
+  drop_fast();
+  std::map<std::string, void *> bw;
+  bool ok = true;
+  auto q4 = [&](const std::string &n, const ggml_tensor *t) {
+    const Ext *e = q4_of(t);
+    ok = ok && e;
+    bw[n] = e ? e->w4 : nullptr;
+  };
+  auto f32 = [&](const std::string &n, const ggml_tensor *t) {
+    char *p = dev_of_t(t);
+    ok = ok && p;
+    bw[n] = p;
+  };
+  q4("gpt_neox.embed_in.weight", M.wte);
+  q4("embed_out.weight", M.lmh);
+  f32("gpt_neox.final_layer_norm.weight", M.lnf_w);
+  f32("gpt_neox.final_layer_norm.bias", M.lnf_b);
+  for (int il = 0; il < (int)M.layers.size(); ++il) {
+    const NeoxLayer &Y = M.layers[il];
+    f32(layer_name(il, "input_layernorm.weight"), Y.ln1_w);
+    f32(layer_name(il, "input_layernorm.bias"), Y.ln1_b);
+    f32(layer_name(il, "post_attention_layernorm.weight"), Y.ln2_w);
+    f32(layer_name(il, "post_attention_layernorm.bias"), Y.ln2_b);
+    q4(layer_name(il, "attention.query.weight"), Y.wq);
+    f32(layer_name(il, "attention.query.bias"), Y.bq);
+    q4(layer_name(il, "attention.key.weight"), Y.wk);
+    f32(layer_name(il, "attention.key.bias"), Y.bk);
+    q4(layer_name(il, "attention.value.weight"), Y.wv);
+    f32(layer_name(il, "attention.value.bias"), Y.bv);
+    q4(layer_name(il, "attention.dense.weight"), Y.wo);
+    f32(layer_name(il, "attention.dense.bias"), Y.bo);
+    q4(layer_name(il, "mlp.dense_h_to_4h.weight"), Y.wfc);
+    f32(layer_name(il, "mlp.dense_h_to_4h.bias"), Y.bfc);
+    q4(layer_name(il, "mlp.dense_4h_to_h.weight"), Y.wproj);
+    f32(layer_name(il, "mlp.dense_4h_to_h.bias"), Y.bproj);
+  }
+  float *kc = (float *)dev_of_t(M.memk), *vc = (float *)dev_of_t(M.memv);
+  if (!ok || !kc || !vc) {
+    set_error("graph fast path: a matched tensor has no device mirror");
+    return VSIM_EINVAL;
+  }
+  const vsim_graph_match_info &I = M.info;
+  vsim_hparams hp{I.n_vocab, I.n_embd, I.n_head, I.n_layer, I.n_rot, 1};
+  vsim_model *m = nullptr;
+  if (int rc = model_create_impl(VSIM_ARCH_GPTNEOX, &hp, I.n_ctx, X.device, 0, I.n_layer, &bw, kc, vc, &m)) return rc;
+  vsim_model_set_mode(m, VSIM_MODE_EXACT);
+  vsim_model_set_graph(m, 1);
+  X.fast.m = m;
+  X.fast.key = plan_key(M);
+  X.fast.gen = X.ext_gen;
+  X.fast.nth = nth;
+  X.fast.scale = M.scale;
+  ++X.fast_plans;
+  return VSIM_OK;
+}
+
+// One fused decode step of a matched graph on the current plan: the logits into the last node.
+int run_fast(const ggml_cgraph *g, const NeoxMatch &M, int nth) {
+  const int32_t tok = M.info.token;
+  if (tok < 0 || tok >= M.info.n_vocab) {
+    set_error("graph fast path: token id out of range");
+    return VSIM_EINVAL;
+  }
+  ggml_tensor *last = g->nodes[g->n_nodes - 1];
+  VSIM_HIP(hipStreamSynchronize(X.stream));  // mirrors uploaded on X.stream are complete
+  if (int rc = model_set_attn(X.fast.m, nth, M.scale)) return rc;
+  if (int rc = vsim_model_eval(X.fast.m, M.info.n_past, &tok, 1, nullptr, nullptr, (float *)last->data)) return rc;
+  X.d2h += (uint64_t)M.info.n_vocab * sizeof(float);
+  X.computes++;
+  X.nodes += g->n_nodes;
+  X.fast_evals++;
+  return VSIM_OK;
+}
+
 struct GgmlContextHead {  // ggml.c:1022-1024, the first fields of struct ggml_context
   size_t mem_size;
   void *mem_buffer;
@@ -393,6 +712,18 @@ int compute(struct ggml_context *ctx, struct ggml_cgraph *g) {
   if (g->n_nodes <= 0) return VSIM_OK;
   if (int rc = ensure_ready()) return rc;
   VSIM_HIP(hipSetDevice(X.device));
+  // an n_threads <= 0 graph runs with 8 threads in the reference (ggml.c:8246-8248)
+  const int nth = g->n_threads > 0 ? g->n_threads : 8;
+  // decode fast path: a recognised single-token gptneox_eval graph on the plan bound to its
+  // tensors (built, after mirroring the leafs, when the weights, the cache or the mirrors change)
+  const ggml_tensor *n0 = g->nodes[0];
+  const bool one_token = !X.fast_off && !X.prof && n0->op == GGML_OP_GET_ROWS && n0->src1 && n0->src1->ne[0] == 1;
+  NeoxMatch M;
+  std::string why;
+  const bool fast = one_token && match_neox_decode(g, M, why);
+  if (fast && X.fast.m && X.fast.gen == X.ext_gen && X.fast.key == plan_key(M)) return run_fast(g, M, nth);
+  if (one_token && !fast && getenv("VSIM_GRAPH_DEBUG"))
+    fprintf(stderr, "vsim_graph_compute: per-node path (%s)\n", why.c_str());
   const GgmlContextHead *h = (const GgmlContextHead *)ctx;
   if (h->mem_buffer != X.arena_host || h->mem_size > X.arena_bytes) {
     if (X.arena_dev) (void)hipFree(X.arena_dev);
@@ -411,8 +742,10 @@ int compute(struct ggml_context *ctx, struct ggml_cgraph *g) {
       if (int rc = register_ext(t)) return rc;
     }
   }
-  // an n_threads <= 0 graph runs with 8 threads in the reference (ggml.c:8246-8248)
-  const int nth = g->n_threads > 0 ? g->n_threads : 8;
+  if (fast) {
+    if (int rc = build_fast(M, nth)) return rc;
+    return run_fast(g, M, nth);
+  }
   for (int i = 0; i < g->n_nodes; ++i)
     if (int rc = node(g->nodes[i], nth, true)) return rc;
   for (int i = 0; i < g->n_leafs; ++i) {
@@ -521,6 +854,9 @@ int vsim_graph_sync_tensor(const struct ggml_tensor *t) {
 
 void vsim_graph_reset(void) {
   std::lock_guard<std::mutex> lk(X.mu);
+  drop_fast();
+  ++X.ext_gen;
+  X.fast_evals = X.fast_plans = 0;
   for (auto &kv : X.ext) {
     if (kv.second.dev) (void)hipFree(kv.second.dev);
     if (kv.second.w4) (void)hipFree(kv.second.w4);
@@ -540,6 +876,24 @@ void vsim_graph_stats(uint64_t *computes, uint64_t *nodes, uint64_t *h2d_bytes, 
   if (nodes) *nodes = X.nodes;
   if (h2d_bytes) *h2d_bytes = X.h2d;
   if (d2h_bytes) *d2h_bytes = X.d2h;
+}
+
+int vsim_graph_match(const struct ggml_cgraph *cgraph, vsim_graph_match_info *info) {
+  if (!cgraph || cgraph->n_nodes <= 0) { set_error("graph_match: empty graph"); return VSIM_EINVAL; }
+  NeoxMatch M;
+  std::string why;
+  if (!match_neox_decode(cgraph, M, why)) {
+    set_error("graph_match: " + why);
+    return VSIM_EINVAL;
+  }
+  if (info) *info = M.info;
+  return VSIM_OK;
+}
+
+void vsim_graph_fast_stats(uint64_t *fast_evals, uint64_t *plans) {
+  std::lock_guard<std::mutex> lk(X.mu);
+  if (fast_evals) *fast_evals = X.fast_evals;
+  if (plans) *plans = X.fast_plans;
 }
 
 int vsim_graph_set_profile(int enable) {

@@ -121,6 +121,12 @@ struct vsim_model {
 
   int graph_mode = -1;
   int graph_kernels = 0;
+  // graph executor's fast path (graph.cpp): weights and KV cache borrowed from its device
+  // mirrors (not freed here), the KQV key grouping of the caller's thread count and the
+  // scale the graph carries (0: computed from the hparams)
+  bool borrowed = false;
+  int kqv_nth = 1;
+  float attn_scale = 0.0f;
   int graph_kernels_kind[4] = {0, 0, 0, 0};  // per decode_graph kind: kernels in one replay
 
   // Per-kernel profiling (bench.py's live roofline): with profiling on, the decode step runs
@@ -957,7 +963,8 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.style = gptj ? 1 : 0;
     A.n_ctx = m->n_ctx;
     A.nsplit = 1;
-    A.scale = scale;
+    A.scale = m->attn_scale != 0.0f ? m->attn_scale : scale;
+    A.kqv_nth = m->kqv_nth;
     A.alibi = bloom ? m->alibi : nullptr;
     A.oq_qs = qa;
     A.oq_d = da;
@@ -1156,8 +1163,15 @@ int vsim_device_count(void) {
 
 size_t vsim_q4_bytes(int rows, int k) { return w4_bytes(rows, k); }
 
-int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
-                      vsim_model **out) {
+}  // extern "C"
+
+namespace vsim {
+// vsim_model_create, or (borrow != null) a whole-model GPT-NeoX / GPT-J executor whose weight
+// slots point at device buffers the caller owns (ggml tensor name -> W4T32 / F32 device
+// pointer, every slot must be there) and whose KV cache is kc / vc ([layer][n_ctx][E] f32):
+// the graph executor's fast path, graph.cpp.
+int model_create_impl(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
+                      const std::map<std::string, void *> *borrow, float *kc, float *vc, vsim_model **out) {
   if (!hp || !out) { set_error("model_create: null argument"); return VSIM_EINVAL; }
   if (arch != VSIM_ARCH_GPTNEOX && arch != VSIM_ARCH_GPTJ && arch != VSIM_ARCH_BLOOM) {
     set_error("model_create: unknown arch");
@@ -1190,27 +1204,48 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
     return fail(hip_fail(hipErrorUnknown, "stream"));
   std::vector<std::pair<std::string, Slot>> plan;
   plan_slots(m, plan);
+  if (borrow) {
+    if (arch == VSIM_ARCH_BLOOM || !kc || !vc) { set_error("model_create: borrowed weights: GPT-NeoX / GPT-J only"); return fail(VSIM_EINVAL); }
+    for (auto &ps : plan) {
+      auto it = borrow->find(ps.first);
+      if (it == borrow->end() || !it->second) {
+        set_error("model_create: borrowed weights: no device buffer for " + ps.first);
+        return fail(VSIM_EINVAL);
+      }
+      ps.second.ptr = it->second;
+      ps.second.loaded = true;
+      m->slots[ps.first] = ps.second;
+    }
+    m->borrowed = true;
+    m->kcache = kc;
+    m->vcache = vc;
+    bind_pointers(m);
+  }
   size_t tot = 0;
   for (auto &ps : plan) tot += (slot_dev_bytes(ps.second) + 255) & ~(size_t)255;
-  // + FD_PAD: the fast GEMV streams whole 16-block batches and zeroes the scales of slots past
-  // a wave's range, so it may read up to 8 KB past a tensor (fast_decode.hip TileStream)
-  if (hipMalloc((void **)&m->warena, tot + FD_PAD) != hipSuccess) { set_error("model_create: weight alloc failed"); return fail(VSIM_ENOMEM); }
-  m->wbytes = tot;
-  size_t off = 0;
-  for (auto &ps : plan) {
-    ps.second.ptr = m->warena + off;
-    off += (slot_dev_bytes(ps.second) + 255) & ~(size_t)255;
-    m->slots[ps.first] = ps.second;
-  }
-  bind_pointers(m);
   const size_t E = hp->n_embd, nl = layer_end - layer_begin;
-  if (hipMalloc((void **)&m->kcache, nl * n_ctx * E * sizeof(float)) != hipSuccess ||
-      hipMalloc((void **)&m->vcache, nl * n_ctx * E * sizeof(float)) != hipSuccess) {
-    set_error("model_create: KV cache alloc failed");
-    return fail(VSIM_ENOMEM);
+  if (!borrow) {
+    // + FD_PAD: the fast GEMV streams whole 16-block batches and zeroes the scales of slots past
+    // a wave's range, so it may read up to 8 KB past a tensor (fast_decode.hip TileStream)
+    if (hipMalloc((void **)&m->warena, tot + FD_PAD) != hipSuccess) { set_error("model_create: weight alloc failed"); return fail(VSIM_ENOMEM); }
+    m->wbytes = tot;
+    size_t off = 0;
+    for (auto &ps : plan) {
+      ps.second.ptr = m->warena + off;
+      off += (slot_dev_bytes(ps.second) + 255) & ~(size_t)255;
+      m->slots[ps.first] = ps.second;
+    }
+    bind_pointers(m);
+    if (hipMalloc((void **)&m->kcache, nl * n_ctx * E * sizeof(float)) != hipSuccess ||
+        hipMalloc((void **)&m->vcache, nl * n_ctx * E * sizeof(float)) != hipSuccess) {
+      set_error("model_create: KV cache alloc failed");
+      return fail(VSIM_ENOMEM);
+    }
+    (void)hipMemset(m->kcache, 0, nl * n_ctx * E * sizeof(float));
+    (void)hipMemset(m->vcache, 0, nl * n_ctx * E * sizeof(float));
+  } else {
+    m->wbytes = tot;
   }
-  (void)hipMemset(m->kcache, 0, nl * n_ctx * E * sizeof(float));
-  (void)hipMemset(m->vcache, 0, nl * n_ctx * E * sizeof(float));
   const int half = hp->n_rot / 2 > 0 ? hp->n_rot / 2 : 1;
   std::vector<double2> cs((size_t)n_ctx * half);
   if (hp->n_rot > 0) rope_table_host(cs.data(), n_ctx, hp->n_rot);
@@ -1233,6 +1268,26 @@ int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   return VSIM_OK;
 }
 
+// The borrowed model's per-call settings: the reference pool's KQV grouping (cgraph->n_threads)
+// and the graph's own attention scale; a change drops the captured decode graphs.
+int model_set_attn(vsim_model *m, int kqv_nth, float scale) {
+  if (kqv_nth < 1) kqv_nth = 1;
+  if (m->kqv_nth == kqv_nth && m->attn_scale == scale) return VSIM_OK;
+  VSIM_HIP(hipStreamSynchronize(m->stream));
+  m->kqv_nth = kqv_nth;
+  m->attn_scale = scale;
+  m->graph_mode = m->graph_am_mode = m->graph_gen_mode = m->graph_st_mode = -1;  // recapture on next use
+  return VSIM_OK;
+}
+}  // namespace vsim
+
+extern "C" {
+
+int vsim_model_create(int arch, const vsim_hparams *hp, int n_ctx, int device, int layer_begin, int layer_end,
+                      vsim_model **out) {
+  return model_create_impl(arch, hp, n_ctx, device, layer_begin, layer_end, nullptr, nullptr, nullptr, out);
+}
+
 void vsim_model_free(vsim_model *m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
@@ -1241,8 +1296,8 @@ void vsim_model_free(vsim_model *m) {
   free_scratch(m);
   free_w16(m);
   if (m->warena) (void)hipFree(m->warena);
-  if (m->kcache) (void)hipFree(m->kcache);
-  if (m->vcache) (void)hipFree(m->vcache);
+  if (m->kcache && !m->borrowed) (void)hipFree(m->kcache);
+  if (m->vcache && !m->borrowed) (void)hipFree(m->vcache);
   if (m->rope_cs) (void)hipFree(m->rope_cs);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   for (hipEvent_t e : m->prof_events) (void)hipEventDestroy(e);
@@ -1250,6 +1305,7 @@ void vsim_model_free(vsim_model *m) {
 }
 
 int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes) {
+  if (m->borrowed) { set_error("set_tensor: the weights belong to the graph executor"); return VSIM_EINVAL; }
   if (!m->w16.empty()) {  // fp16 weight images are remade from the new weights on next use
     (void)hipStreamSynchronize(m->stream);
     free_w16(m);
@@ -1316,6 +1372,7 @@ int vsim_model_get_tensor(vsim_model *m, const char *name, void *host, size_t nb
 }
 
 int vsim_model_randomize(vsim_model *m, uint64_t seed, float stddev) {
+  if (m->borrowed) { set_error("randomize: the weights belong to the graph executor"); return VSIM_EINVAL; }
   VSIM_HIP(hipSetDevice(m->device));
   if (!m->w16.empty()) {
     VSIM_HIP(hipStreamSynchronize(m->stream));
