@@ -180,6 +180,24 @@ def gen_alibi():
     np.savez_compressed(os.path.join(OUT, "ops_attnsm_alibi.npz"), **cases)
 
 
+def gen_prompt_mulmat():
+    """Q4_0 x F32 mul_mat of the reference (ggml.c:4891-5165: INIT re-quantizes the N activation
+    rows, COMPUTE the imax.c:1182-1230 dot chains) at prompt shapes, N >= 256 tokens: the cases of
+    golden_util.PROMPT_MULMAT_CASES.  Stored: shape, seed, sha256 of the regenerated inputs, y."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_util as gu
+    cases = {}
+    for ci, (M, K, N, seed) in enumerate(gu.PROMPT_MULMAT_CASES):
+        w, xa = gu.prompt_mulmat_inputs(M, K, N, seed)
+        w.tofile(tmp("w")); xa.tofile(tmp("x"))
+        harness("mulmat", M, K, N, tmp("w"), tmp("x"), tmp("y"))
+        cases[f"c{ci}_shape"] = np.array([M, K, N, seed], np.int64)
+        cases[f"c{ci}_sha"] = np.array(gu.inputs_sha(w, xa))
+        cases[f"c{ci}_y"] = fread(tmp("y"), np.float32)
+        print("prompt mulmat", M, K, N)
+    np.savez_compressed(os.path.join(OUT, "ops_mulmat_prompt.npz"), **cases)
+
+
 def run_vsim(model, prompt, extra):
     cmd = [VSIM, "gptneox", "-m", model, "--prompt", prompt, "--threads", "1", *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, check=True)
@@ -237,7 +255,11 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["alibi"]:  # (added later: regenerates only the ALiBi vectors)
         gen_alibi()
         sys.exit(0)
+    if sys.argv[1:] == ["prompt_mulmat"]:  # (added in r03: only the prompt-shape mul_mat vectors)
+        gen_prompt_mulmat()
+        sys.exit(0)
     gen_ops()
     gen_alibi()
+    gen_prompt_mulmat()
     gen_e2e()
     print("fixtures written to", OUT)

@@ -53,3 +53,26 @@ def fmt8(v) -> list[str]:
 
 def prompt_ids(p: str):
     return [int(t) for t in p.split()]
+
+
+# Prompt-shape Q4_0 mul_mat vectors (ops_mulmat_prompt.npz): the fixture holds the seeds and the
+# reference's outputs only; the inputs are regenerated here (PCG64) and checked against the
+# sha256 the generator recorded.
+PROMPT_MULMAT_CASES = [  # (M rows, K, N tokens, seed): GPT-J / codegen-16B prompt widths
+    (256, 4096, 256, 101), (192, 6144, 320, 102), (96, 24576, 256, 103)]
+
+
+def prompt_mulmat_inputs(M, K, N, seed):
+    """(Q4_0 AoS weight bytes [M][K], f32 activations [N][K]) for one case: weights N(0, 0.02)
+    quantized with quantize_row_q4_0 semantics, activations N(0, 1) with exact zeros and tiny
+    values mixed in (as the op goldens' activ())."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    w = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))
+    x = rng.standard_normal(N * K).astype(np.float32)
+    x[rng.integers(0, N * K, size=N * K // 97)] = 0.0
+    x[rng.integers(0, N * K, size=N * K // 61)] *= np.float32(1e-7)
+    return w, x.astype(np.float32)
+
+
+def inputs_sha(w, x) -> str:
+    return hashlib.sha256(np.ascontiguousarray(w).tobytes() + np.ascontiguousarray(x).tobytes()).hexdigest()

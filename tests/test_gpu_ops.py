@@ -256,6 +256,47 @@ def test_prefill_gemm_f16(M, K, N):
     assert np.all(np.abs(y - ref) <= 2.0 ** -10 * absum + 1e-5 * (np.abs(b) + 1))
 
 
+@pytest.mark.parametrize("c", cases(ops("mulmat_prompt")), ids=lambda c: "x".join(map(str, c["shape"][:3])))
+def test_prompt_gemm_vs_reference_mul_mat(c):
+    """Both prompt GEMM paths against the REFERENCE's Q4_0 mul_mat output at prompt shapes
+    (tests/golden/ops_mulmat_prompt.npz: ggml.c:4891-5165 at N >= 256, K = 4096 / 6144 / 24576):
+      * exact mode (the chain GEMV over N rows, k_gemv_exact_rows): bit-identical;
+      * the long-prompt fast path the model runs for N >= 256 (vsim_op_act_quant_f16 -> the
+        W4T32 weight -> fp16 MFMA GEMM with fp32 accumulation, gemm_f16.hip): per element
+          |y - y_ref| <= (2^-10 + 1.5 K 2^-24) * sum_k |w_k x_k|
+        (w, x the Q4_0 values d*(q-8)): each fp16 operand carries <= 2^-11 relative rounding,
+        the reference's K/2-add fp32 chain and our fp32 accumulation <= (K/2 + K) 2^-24 each.
+        This bound is derived, not fitted; the measured maximum is printed."""
+    import golden_util as gu
+    M, K, N, seed = (int(v) for v in c["shape"])
+    w_aos, x = gu.prompt_mulmat_inputs(M, K, N, seed)
+    assert gu.inputs_sha(w_aos, x) == str(c["sha"])
+    y_ref = c["y"].reshape(N, M)
+    w = repack(w_aos, M, K)
+    xq, xd = quantize(x, K, N)
+    y = gemv(w, M, K, xq, xd, N, hip.MODE_EXACT).reshape(N, M)
+    assert np.array_equal(bits(y), bits(y_ref)), "exact prompt GEMV"
+    # the fast path, as the model's long-prompt layer calls it
+    x16 = torch.empty(N * K, dtype=torch.float16, device=DEV)
+    hip.check(hip.lib().vsim_op_act_quant_f16(dev(x).data_ptr(), K, N, None, 0, x16.data_ptr(), None), "act_quant")
+    img = torch.empty(M * K, dtype=torch.float16, device=DEV)
+    hip.check(hip.lib().vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    yf = torch.empty(N * M, dtype=torch.float32, device=DEV)
+    hip.check(hip.lib().vsim_op_gemm_f16(img.data_ptr(), M, K, x16.data_ptr(), N, None, yf.data_ptr(), None), "gemm")
+    yf = host(yf).reshape(N, M)
+    xq_aos = torch.empty(N * K // 32 * 20, dtype=torch.uint8, device=DEV)
+    hip.check(hip.lib().vsim_op_act_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
+    W = np.abs(mg.dequantize_q4_0(w_aos, K).astype(np.float64))
+    X = np.abs(mg.dequantize_q4_0(host(xq_aos), K).astype(np.float64))
+    absum = X @ W.T
+    bound = (2.0 ** -10 + 1.5 * K * 2.0 ** -24) * absum
+    err = np.abs(yf.astype(np.float64) - y_ref)
+    ratio = float(np.max(err / np.maximum(absum, 1e-30)))
+    print(f"{M}x{K}x{N}: max |y - y_ref| / sum|w x| = {ratio:.3g} (bound {2.0 ** -10 + 1.5 * K * 2.0 ** -24:.3g})")
+    bad = err > bound
+    assert not bad.any(), f"{bad.sum()} elements outside the bound, worst ratio {ratio:.3g}"
+
+
 @pytest.mark.parametrize("M,K,N", [(520, 512, 300), (256, 64, 256), (1000, 128, 600), (3072, 1024, 512),
                                    (300, 4096, 257), (24576, 64, 2048)])
 def test_prefill_gemm_f16_256(M, K, N):

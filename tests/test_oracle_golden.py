@@ -28,6 +28,17 @@ def test_mul_mat_q4_0(c):
     assert np.array_equal(bits(O.mul_mat(c["w"], M, K, c["x"], N, nthreads=5)), bits(c["y"]))
 
 
+@pytest.mark.parametrize("c", cases(ops("mulmat_prompt")), ids=lambda c: "x".join(map(str, c["shape"][:3])))
+def test_mul_mat_q4_0_prompt_shapes(c):
+    """The reference's Q4_0 mul_mat at prompt shapes (N >= 256 tokens, K up to 4 x 6144),
+    inputs regenerated from the fixture's seed (sha256 checked)."""
+    import golden_util as gu
+    M, K, N, seed = (int(v) for v in c["shape"])
+    w, x = gu.prompt_mulmat_inputs(M, K, N, seed)
+    assert gu.inputs_sha(w, x) == str(c["sha"])
+    assert np.array_equal(bits(O.mul_mat(w, M, K, x, N, nthreads=8)), bits(c["y"]))
+
+
 @pytest.mark.parametrize("c", cases(ops("norm")), ids=lambda c: "x".join(map(str, c["shape"])))
 def test_norm(c):
     n, r = (int(v) for v in c["shape"])

@@ -40,8 +40,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--a", type=int, default=8)
-    ap.add_argument("--b", type=int, default=264)
-    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--b", type=int, default=488)
+    ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     arch, hp = mg.CONFIGS["pythia-12b"]
@@ -56,14 +56,15 @@ def main():
     streams = {}
     env = dict(os.environ, VSIM_GRAPH_STATS="1")
     for name, exe in (("graph", GRAPH), ("vsim_hip", HIP)):
-        best = None
-        for _ in range(a.reps):
+        runs = []
+        for _ in range(a.reps):  # (the two binaries alternate within a rep: same box state)
             ta, _, _ = timed(exe, path, a.a, env)
             tb, toks, err = timed(exe, path, a.b, env)
             tps = (a.b - a.a) / (tb - ta)
-            best = tps if best is None else max(best, tps)
+            runs.append(tps)
             print(f"{name}: {tps:.1f} tok/s ({a.b - a.a} tokens in {tb - ta:.3f} s)", file=sys.stderr, flush=True)
-        res[name] = round(best, 2)
+        res[name] = round(sorted(runs)[len(runs) // 2], 2)  # median
+        res[name + "_runs"] = [round(v, 1) for v in runs]
         streams[name] = toks
         if name == "graph":
             res["graph_stats"] = [ln for ln in err.splitlines() if "fast path" in ln][-1:]
@@ -71,6 +72,7 @@ def main():
         "what": "decode tok/s, reference eval loop (vsim.cpp + ggml graph) on vsim_graph_compute vs vsim-hip",
         "model": f"pythia-12b width (E={hp.n_embd}, H={hp.n_head}, V={hp.n_vocab}), {a.layers} layers, synthetic",
         "tokens": a.b - a.a, "graph_tok_s": res["graph"], "vsim_hip_tok_s": res["vsim_hip"],
+        "runs": {"graph": res["graph_runs"], "vsim_hip": res["vsim_hip_runs"]}, "statistic": "median of reps",
         "ratio": round(res["graph"] / res["vsim_hip"], 4), "streams_equal": streams["graph"] == streams["vsim_hip"],
         "graph_stats": res["graph_stats"],
     }
