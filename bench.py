@@ -117,6 +117,18 @@ def metric_name(config: str) -> str:
 
 def q4_weight_bytes(arch: str, hp: mg.HParams) -> float:
     """B_w per decode token: every Q4_0 matrix incl. lm_head, 0.625 B/w."""
+    exact = None
+    if args.prefill_exact:
+        model.set_mode(hip.MODE_EXACT)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        model.eval(0, ids)
+        torch.cuda.synchronize()
+        te = time.perf_counter() - t0
+        model.set_mode(hip.MODE_FAST)
+        exact = {"ms_per_prompt": round(te * 1e3, 1), "value": round(N / te, 1), "unit": "tokens/s",
+                 "path": "exact mode: per-token fp32 chains (the reference's sumf order), bit-identical to the oracle",
+                 "steps": 1}
     E, F, L, V = hp.n_embd, hp.n_ff, hp.n_layer, hp.n_vocab
     return 0.625 * (L * (4 * E * E + 2 * E * F) + V * E)
 
@@ -357,10 +369,12 @@ def pipeline_companion(args, world, rank, local, steps=64, warmup=8, limit=300):
 
 def run_prefill(args, dev):
     """One prompt eval of args.prefill tokens (codegen-16B, N = 2048) in
-    fast mode: every Q4_0 matmul on fp16 MFMA (gemm_f16.hip: for N >= 256 the 256 x 256-tile
-    GEMM on fp16 images of the weights, made on the first prompt and kept), attention on the
-    fp16 MFMA prefill kernel, the elementwise ops on the general-path kernels.  `value` is the
-    steady state; the first prompt, which also expands the weights, is reported beside it."""
+    fast mode: every Q4_0 matmul on fp16 MFMA after in-LDS dequant (gemm_f16.hip: for N >= 256
+    the 256 x 256-tile GEMM reading the W4T32 weights, no fp16 image), attention on the fp16
+    MFMA prefill kernel, the elementwise ops fused into the GEMM epilogues or on the
+    general-path kernels.  `value` is the steady state; the first prompt is reported beside it.
+    --prefill-exact also times the same prompt on the exact path (the reference's fp32 chains,
+    bit-identical to the oracle) and reports it as `exact_mode`."""
     import torch
     arch_s, hp = mg.CONFIGS[args.config]
     arch = ARCHS[arch_s]
@@ -394,12 +408,13 @@ def run_prefill(args, dev):
         "value": round(N / dt, 1), "unit": "tokens/s", "n_gpus": 1, "steps": reps,
         "ms_per_prompt": round(dt * 1e3, 2), "higher_is_better": True,
         "first_prompt_ms": round(first * 1e3, 2),
-        "weight_images_GB": round(2.0 * L * (4 * E * E + 2 * E * F) / 1e9, 2) if N >= 256 else 0.0,
+        "weight_images_GB": 0.0,  # (r03: the GEMM dequantizes the Q4_0 weights in LDS, no fp16 copies)
         "dtype": "f16 MFMA, f32 accumulate", "data": "synthetic (random-init weights, drawn on device)",
         "config": {"workload": f"{args.config} prompt eval, N={N}", "mode": "fast"},
         "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": 2500.0, "unit": "TFLOP/s",
                      "frac": round(tflops / 2500.0, 4), "traffic": None,
                      "flops": {"gemm": gemm_flops, "attention": attn_flops}},
+        "exact_mode": exact,
     }), flush=True)
 
 
@@ -419,6 +434,8 @@ def main():
                     help="split the layers over the ranks (one residual send per stage boundary per token)")
     ap.add_argument("--prefill", type=int, default=0,
                     help="time one prompt eval of this many tokens instead of decode (fast-mode fp16 MFMA GEMM)")
+    ap.add_argument("--prefill-exact", action="store_true",
+                    help="with --prefill: also time the prompt once on the exact (oracle-identical) path")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: host-staged sends, for rehearsing the pipeline with ranks sharing a GPU")
     ap.add_argument("--no-pipeline-20b", action="store_true",

@@ -105,7 +105,7 @@ void vsim_graph_stats(uint64_t *computes, uint64_t *nodes, uint64_t *h2d_bytes, 
 int vsim_graph_set_profile(int enable);
 int vsim_graph_profile_report(char *buf, size_t cap);
 /* Decode fast path of vsim_graph_compute.  A single-token eval of gptneox_eval
- * (vsim.cpp:470-747, use_parallel_residual = 1) is recognised node by node (52 nodes per
+ * (vsim.cpp:470-747, use_parallel_residual = 1) is recognised node by node (42 nodes per
  * layer in ggml_build_forward_expand order, plus get_rows and the final norm + lm_head) and
  * runs as the model executor's fused decode step -- 3 launches per layer, replayed as one
  * hipGraph -- on the weights and KV cache the per-node path mirrored, with the KQV grouping of
@@ -117,7 +117,7 @@ typedef struct {
   int32_t n_layer, n_embd, n_head, n_rot, n_vocab, n_ctx, n_past, token;
 } vsim_graph_match_info;
 int vsim_graph_match(const struct ggml_cgraph *cgraph, vsim_graph_match_info *info);
-/* evals that took the fast path, and fast-path plans built (one per weight set / n_threads) */
+/* evals that took the fast path, and fast-path plans built (one per set of weight tensors) */
 void vsim_graph_fast_stats(uint64_t *fast_evals, uint64_t *plans);
 /* drop-in statistics: calls, bytes moved host<->device, device weight-cache size */
 void vsim_dropin_stats(uint64_t *calls, uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *cached_bytes);
@@ -160,6 +160,13 @@ int vsim_op_gemm_f16_rope(const void *w16, int M, int K, const void *x16, int n,
                           const double *cs, int d, int n_rot, int p0, void *stream);
 int vsim_op_gemm_f16_join(const void *w16, int M, int K, const void *x16, int n, const float *bias, float *res,
                           const float *res_a, void *stream);
+/* The model's long-prompt GEMM: the products of vsim_op_gemm_f16* straight from the W4T32
+ * weight w, dequantized in LDS to the same fp16 halves (no image).  Epilogue, one at a time:
+ * q16 != NULL the GELU-quantize one (y unused, bias required), cs != NULL the RoPE one into y,
+ * join != 0 the residual join in place (y = res, res_a as in vsim_op_gemm_f16_join); else the
+ * plain store (+ bias). */
+int vsim_op_gemm_q4_256(const void *w, int M, int K, const void *x16, int n, const float *bias, float *y, void *q16,
+                        const double *cs, int d, int n_rot, int p0, int join, const float *res_a, void *stream);
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream);
 /* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);

@@ -261,8 +261,9 @@ def test_prompt_gemm_vs_reference_mul_mat(c):
     """Both prompt GEMM paths against the REFERENCE's Q4_0 mul_mat output at prompt shapes
     (tests/golden/ops_mulmat_prompt.npz: ggml.c:4891-5165 at N >= 256, K = 4096 / 6144 / 24576):
       * exact mode (the chain GEMV over N rows, k_gemv_exact_rows): bit-identical;
-      * the long-prompt fast path the model runs for N >= 256 (vsim_op_act_quant_f16 -> the
-        W4T32 weight -> fp16 MFMA GEMM with fp32 accumulation, gemm_f16.hip): per element
+      * the long-prompt fast path the model runs for N >= 256 (vsim_op_act_quant_f16, then
+        vsim_op_gemm_q4_256: the W4T32 weight dequantized to fp16 in LDS, fp16 MFMA, fp32
+        accumulation, gemm_f16.hip): per element
           |y - y_ref| <= (2^-10 + 1.5 K 2^-24) * sum_k |w_k x_k|
         (w, x the Q4_0 values d*(q-8)): each fp16 operand carries <= 2^-11 relative rounding,
         the reference's K/2-add fp32 chain and our fp32 accumulation <= (K/2 + K) 2^-24 each.
@@ -276,13 +277,12 @@ def test_prompt_gemm_vs_reference_mul_mat(c):
     xq, xd = quantize(x, K, N)
     y = gemv(w, M, K, xq, xd, N, hip.MODE_EXACT).reshape(N, M)
     assert np.array_equal(bits(y), bits(y_ref)), "exact prompt GEMV"
-    # the fast path, as the model's long-prompt layer calls it
+    # the fast path, as the model's long-prompt layer calls it (the GEMM on the W4T32 weight)
     x16 = torch.empty(N * K, dtype=torch.float16, device=DEV)
     hip.check(hip.lib().vsim_op_act_quant_f16(dev(x).data_ptr(), K, N, None, 0, x16.data_ptr(), None), "act_quant")
-    img = torch.empty(M * K, dtype=torch.float16, device=DEV)
-    hip.check(hip.lib().vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
     yf = torch.empty(N * M, dtype=torch.float32, device=DEV)
-    hip.check(hip.lib().vsim_op_gemm_f16(img.data_ptr(), M, K, x16.data_ptr(), N, None, yf.data_ptr(), None), "gemm")
+    hip.check(hip.lib().vsim_op_gemm_q4_256(w.data_ptr(), M, K, x16.data_ptr(), N, None, yf.data_ptr(), None, None,
+                                            0, 0, 0, 0, None, None), "gemm")
     yf = host(yf).reshape(N, M)
     xq_aos = torch.empty(N * K // 32 * 20, dtype=torch.uint8, device=DEV)
     hip.check(hip.lib().vsim_op_act_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
@@ -393,6 +393,55 @@ def test_prefill_gemm_gelu_epilogue_bit_identical(M, K, N):
     hip.check(L.vsim_op_gemm_f16_gelu_q(w.data_ptr(), M, K, x.data_ptr(), N, bd.data_ptr(), got.data_ptr(), None), "gq")
     torch.cuda.synchronize()
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,K,N", [(520, 512, 300), (256, 64, 256), (1056, 128, 600), (3072, 1024, 512),
+                                   (300, 4096, 257), (24576, 64, 2048), (6144, 6144, 2048)])
+def test_prefill_gemm_q4_in_lds_dequant_bit_identical(M, K, N):
+    """The long-prompt GEMM the model runs (vsim_op_gemm_q4_256: the W4T32 weight's raw blocks
+    loaded two K-tiles ahead and dequantized in LDS, no fp16 image) gives the bits of the image
+    GEMM (k_w4_expand_f16 + vsim_op_gemm_f16*) for every epilogue: plain (+bias), GELU-quantize,
+    GPT-J RoPE, residual join.  Ragged M / N, one and two K-tiles, both tile heights (AP 3 / 4,
+    launch_gemm_f16_256's choice), the codegen-16B square shape."""
+    rng = np.random.default_rng(5 * M + K + N)
+    w_aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05))
+    w = repack(w_aos, M, K)
+    img = torch.empty(M * K, dtype=torch.float16, device=DEV)
+    L = hip.lib()
+    hip.check(L.vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    x = torch.from_numpy((rng.standard_normal((N, K)) * 0.5).astype(np.float16)).to(DEV)
+    bd = dev((rng.standard_normal(M) * 0.1).astype(np.float32))
+
+    def both(fn_img, fn_q4, out_dtype=torch.float32, init=None):
+        a = torch.empty(N * M, dtype=out_dtype, device=DEV) if init is None else init.clone()
+        b = torch.empty(N * M, dtype=out_dtype, device=DEV) if init is None else init.clone()
+        hip.check(fn_img(a), "image path")
+        hip.check(fn_q4(b), "q4 path")
+        torch.cuda.synchronize()
+        assert torch.equal(a.view(torch.int32 if out_dtype == torch.float32 else torch.int16),
+                           b.view(torch.int32 if out_dtype == torch.float32 else torch.int16))
+
+    xp, wp, ip, bp = x.data_ptr(), w.data_ptr(), img.data_ptr(), bd.data_ptr()
+    both(lambda y: L.vsim_op_gemm_f16(ip, M, K, xp, N, bp, y.data_ptr(), None),
+         lambda y: L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, y.data_ptr(), None, None, 0, 0, 0, 0, None, None))
+    if M % 32 == 0:
+        both(lambda q: L.vsim_op_gemm_f16_gelu_q(ip, M, K, xp, N, bp, q.data_ptr(), None),
+             lambda q: L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, None, q.data_ptr(), None, 0, 0, 0, 0, None, None),
+             out_dtype=torch.float16)
+    if M % 256 == 0:
+        d, n_rot, p0 = 256, 64, 3
+        half = n_rot // 2
+        theta = np.arange(p0 + N, dtype=np.float64)[:, None] * 10000.0 ** (-2.0 * np.arange(half) / n_rot)[None, :]
+        cs = dev(np.ascontiguousarray(np.stack([np.cos(theta), np.sin(theta)], axis=-1)))
+        both(lambda y: L.vsim_op_gemm_f16_rope(ip, M, K, xp, N, bp, y.data_ptr(), cs.data_ptr(), d, n_rot, p0, None),
+             lambda y: L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, y.data_ptr(), None, cs.data_ptr(), d, n_rot, p0, 0,
+                                             None, None))
+    if M % 4 == 0:
+        R = dev(rng.standard_normal(N * M).astype(np.float32))
+        A = dev(rng.standard_normal(N * M).astype(np.float32))
+        both(lambda r: L.vsim_op_gemm_f16_join(ip, M, K, xp, N, bp, r.data_ptr(), A.data_ptr(), None),
+             lambda r: L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, r.data_ptr(), None, None, 0, 0, 0, 1, A.data_ptr(),
+                                             None), init=R)
 
 
 @pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])

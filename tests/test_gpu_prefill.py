@@ -63,7 +63,7 @@ def test_exact_prompt_bit_exact_vs_oracle(cfg, N, tmp_path):
 
 
 @pytest.mark.parametrize("cfg", ["small-gptj", "small-neox", "small-bloom"])
-@pytest.mark.parametrize("N", [72, 288])  # 288: the 256 x 256-tile GEMM on the fp16 weight images
+@pytest.mark.parametrize("N", [72, 288])  # 288: the 256 x 256-tile GEMM, weights dequantized in LDS
 def test_fast_prompt_vs_oracle(cfg, N, tmp_path):
     arch, hp, path, om = _model_pair(cfg, tmp_path)
     res = []

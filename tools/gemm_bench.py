@@ -1,29 +1,48 @@
-"""Long-prompt GEMM timing (k_gemm_f16_256 via vsim_op_gemm_f16) at the codegen-16B shapes
-(N = 2048): TFLOP/s per shape, HIP events over repeated launches."""
+"""Long-prompt GEMM timing at the codegen-16B shapes (N = 2048): TFLOP/s per shape, HIP events
+over repeated launches, for the model's kernel (vsim_op_gemm_q4_256: the W4T32 weight
+dequantized in LDS) and the fp16-image kernel it replaced (vsim_op_gemm_f16 on k_w4_expand_f16's
+image), on the same weights."""
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vsim_amd import hip  # noqa: E402
+from vsim_amd import modelgen as mg  # noqa: E402
 
-N = 2048
+N = int(os.environ.get("GEMM_N", "2048"))
 shapes = [(6144, 6144), (24576, 6144), (6144, 24576)]
-for M, K in shapes:
-    w = torch.empty(M * K, dtype=torch.float16, device="cuda").normal_(0, 0.05)
-    x = torch.empty(N * K, dtype=torch.float16, device="cuda").normal_(0, 0.5)
-    y = torch.empty(N * M, dtype=torch.float32, device="cuda")
-    f = lambda: hip.check(hip.lib().vsim_op_gemm_f16(w.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None), "g")
+L = hip.lib()
+
+
+def timeit(f, reps=20):
     for _ in range(3):
         f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 20
     e0.record()
     for _ in range(reps):
         f()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    print(f"M={M} K={K} N={N}: {ms * 1e3:.1f} us  {2.0 * M * K * N / ms / 1e9:.0f} TFLOP/s", flush=True)
+    return e0.elapsed_time(e1) / reps
+
+
+rng = np.random.default_rng(0)
+for M, K in shapes:
+    aos = torch.from_numpy(mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))).cuda()
+    w = torch.empty(hip.q4_bytes(M, K), dtype=torch.uint8, device="cuda")
+    hip.check(L.vsim_op_q4_repack(aos.data_ptr(), w.data_ptr(), M, K, None), "repack")
+    img = torch.empty(M * K, dtype=torch.float16, device="cuda")
+    hip.check(L.vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    x = torch.empty(N * K, dtype=torch.float16, device="cuda").normal_(0, 0.5)
+    y = torch.empty(N * M, dtype=torch.float32, device="cuda")
+    fq = lambda: hip.check(L.vsim_op_gemm_q4_256(w.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None, None,
+                                                 0, 0, 0, 0, None, None), "q4")
+    fi = lambda: hip.check(L.vsim_op_gemm_f16(img.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None), "img")
+    for name, f in (("q4 in-LDS dequant", fq), ("fp16 image", fi)):
+        ms = timeit(f)
+        print(f"M={M} K={K} N={N} {name:18s}: {ms * 1e3:.1f} us  {2.0 * M * K * N / ms / 1e9:.0f} TFLOP/s", flush=True)
+    del aos, w, img, x, y

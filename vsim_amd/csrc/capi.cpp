@@ -85,6 +85,29 @@ int vsim_op_gemm_f16_join(const void *w16, int M, int K, const void *x16, int n,
   e.res_a = res_a;
   return launch_gemm_f16_256(w16, M, K, x16, n, bias, res, (hipStream_t)stream, nullptr, &e);
 }
+int vsim_op_gemm_q4_256(const void *w, int M, int K, const void *x16, int n, const float *bias, float *y, void *q16,
+                        const double *cs, int d, int n_rot, int p0, int join, const float *res_a, void *stream) {
+  if (!w || !x16 || (!q16 && !y) || M <= 0 || K <= 0 || K % QK || p0 < 0) {
+    set_error("gemm_q4_256: bad argument");
+    return VSIM_EINVAL;
+  }
+  if ((q16 != nullptr) + (cs != nullptr) + (join != 0) > 1) {
+    set_error("gemm_q4_256: one epilogue at a time (q16, cs or join)");
+    return VSIM_EINVAL;
+  }
+  G2Epi e;
+  if (cs) {
+    e.cs = (const double2 *)cs;
+    e.d = d;
+    e.n_rot = n_rot;
+    e.p0 = p0;
+  } else if (join) {
+    e.res = y;
+    e.res_a = res_a;
+  }
+  return launch_gemm_q4_256(w4_view(w, M, K), x16, n, bias, q16 ? nullptr : y, (hipStream_t)stream, q16,
+                            cs || join ? &e : nullptr);
+}
 int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, float *y, void *stream) {
   return launch_get_rows(w, K, V, rows, n, y, (hipStream_t)stream);
 }

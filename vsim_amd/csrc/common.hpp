@@ -270,8 +270,6 @@ int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, flo
 #define VSIM_G2_MIN_N 256
 #endif
 constexpr int G2_MIN_N = VSIM_G2_MIN_N;
-// free device memory the fp16 weight images always leave (model.cpp g2_image)
-constexpr size_t W16_HEADROOM = (size_t)16 << 30;
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
 // q16 non-null: y is not written; bias + GELU + Q4_0 quantize of the result into q16 ([n][M]
 // fp16 values d*(q-8), the next GEMM's operand, as launch_act_quant_f16(y, ..., gelu) makes)
@@ -290,6 +288,10 @@ struct G2Epi {
   _Float16 *h16 = nullptr;
   int h16_ld = 0, h16_t = 0;
 };
+// the same GEMM straight from the W4T32 weight (dequantized to the same fp16 halves in LDS, no
+// image): what the model runs for N >= G2_MIN_N
+int launch_gemm_q4_256(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s,
+                       void *q16 = nullptr, const G2Epi *epi = nullptr);
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
                         hipStream_t s, void *q16 = nullptr, const G2Epi *epi = nullptr);
 bool attn_prefill_supported(int d);

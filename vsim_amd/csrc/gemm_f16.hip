@@ -210,7 +210,8 @@ __global__ void __launch_bounds__(GM_THREADS) k_gemm_q4_f16(W4 W, const _Float16
 // N = 2048 is 192 tiles of 256 rows but 256 tiles of 192), 8 waves: 2 along M x 4 along N,
 // (BM/2) x 64 each, v_mfma_f32_16x16x32_f16, K in tiles of 64.  LDS: two buffers x {AP A
 // pieces, 4 B pieces} of 8 KB ([64 rows][64 halves], 16-byte chunks XOR-swizzled by
-// (row >> 1) & 7 so the 16 lanes of a ds_read_b128 group hit 16 different bank slots; the DMA
+// row & 7 so the 16 lanes of a ds_read_b128 group hit 16 different bank slots (and the 8 lanes
+// of a ds_write_b128 group of the Q4A dequant 8 different 16-byte slots of the 32 banks); the DMA
 // is lane-linear, the swizzle is on its source address).  Each K-tile is 4 phases, one output
 // quadrant ((BM/4) x 32 per wave) per phase; a phase is {LDS reads, DMA issue} barrier {MFMAs}
 // barrier.  The two wave groups (A rows [0, BM/2) and [BM/2, BM); one wave of each per SIMD)
@@ -251,12 +252,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // 32-row block of one column n sits in 4 lanes (fk = 0..3) x 8 registers of two accumulators.
 // EM: the f32 epilogue's extra work (G2Epi): 0 none, 1 RoPE (+ the fp16 row copy), 2 residual
 // join, 3 the fp16 transposed copy.
-template <bool GQ, int AP, int EM>
+// Q4A: the weight operand is the W4T32 Q4_0 weight WQ itself (0.625 B per weight from HBM, no
+// fp16 image): each K-tile's raw blocks are loaded into registers in P2 two tiles ahead (one
+// Q4_0 block of one row per thread: 16 nibble bytes + the scale, a wave = one 32-row tile's two
+// blocks, 1 KB + 256 B contiguous) and in P1 of the tile before their use dequantized with
+// deq_block_f16 -- the same fp16 halves k_w4_expand_f16 writes -- into the A pieces of the LDS
+// buffer, where the DMA of the image path would have put them (same swizzle, same reads).
+template <bool GQ, int AP, int EM, bool Q4A = false>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
                                                                  const _Float16 *__restrict__ B, int N,
                                                                  const float *__restrict__ bias, float *__restrict__ Y,
                                                                  const uint16_t *__restrict__ gelu_tab,
-                                                                 _Float16 *__restrict__ Q16, const G2Epi epi) {
+                                                                 _Float16 *__restrict__ Q16, const G2Epi epi,
+                                                                 const W4 WQ) {
   constexpr int BM = 64 * AP, MR = 2 * AP;  // tile rows; 16-row M-reps per wave
   constexpr int NPC = AP + 4;               // pieces per buffer
   extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
@@ -276,10 +284,62 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     const int kc = min(kt, nk - 1);
     const bool isA = p < AP;
     const int r = wave * 8 + (lane >> 3);        // this lane's row within the piece
-    const int c = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at LDS chunk lane & 7
+    const int c = (lane & 7) ^ (r & 7);  // logical chunk stored at LDS chunk lane & 7
     const int grow = min((isA ? m0 + p * 64 : n0 + (p - AP) * 64) + r, (isA ? M : N) - 1);
     const _Float16 *g = (isA ? A : B) + (size_t)grow * K + (size_t)kc * G2_BK + 8 * c;
     glds16<false>(g, lbase + (uint32_t)((((kt & 1) * NPC + p) * G2_PIECE + wave * 8 * G2_BK) * 2));
+  };
+  // Q4A: this thread's unit of a K-tile: 32-row tile ut of the BM rows (its wave), block ub of
+  // the tile's two, row ur of the 32 (the lane); waves past the tile's 32-row tiles take none
+  const int ut = wave, ub = lane >> 5, ur = lane & 31;
+  const bool qown = Q4A && ut < BM / T32;
+  const int qnb = K / QK, qtiles = (M + T32 - 1) / T32;
+  const int qtile = min(m0 / T32 + ut, qtiles - 1);  // clamped: the rows past M are not stored
+  [[maybe_unused]] u32x4 qraw = {0u, 0u, 0u, 0u}, qraw_n = {0u, 0u, 0u, 0u};  // tile t+1's unit, tile t+2's
+  [[maybe_unused]] float qd = 0.0f, qd_n = 0.0f;
+  // (inline asm, like the DMA: the compiler's wait-count bookkeeping would put a vmcnt(0) in
+  // front of the first use, which also waits for the B pieces staged after these loads; they
+  // are retired by the explicit vmcnt(0) of P4 in the tile before their use)
+  auto qload = [&](int kt, u32x4 &r, float &rd) {  // raw block (2 kt + ub) of row ur of tile qtile
+    if (!qown) return;
+    const size_t o = ((size_t)qtile * qnb + 2 * min(kt, nk - 1) + ub) * T32 + ur;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(WQ.qs + o * 16) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(rd) : "v"(WQ.d + o) : "memory");
+  };
+  auto qstore = [&](int buf) {  // dequantize the unit into the A pieces of `buf`
+    if (!qown) return;
+    half8 h[4];
+    deq_block_f16(make_uint4(qraw[0], qraw[1], qraw[2], qraw[3]), qd, h);
+    const int row = ut * T32 + ur;
+    _Float16 *base = g2lds + buf * NPC * G2_PIECE + row * G2_BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(half8 *)(base + 8 * ((4 * ub + j) ^ (row & 7))) = h[j];
+  };
+  // one word (8 values) of the unit: deq_block_f16's arithmetic for word w, stored to its chunk
+  // (scalar v_fma_f32, not the packed form deq_block_f16 uses: beside MFMAs a v_pk_fma_f32
+  // costs ~22 cycles more than two v_fma_f32, MI355X_MICROARCH.md; same values: fma(n 2^-9,
+  // 512 d, -8 d) rounds d (n - 8) once, then once more to fp16)
+  auto qstore_word = [&](int buf, int w) {
+    if (!qown) return;
+    const float d512 = 512.0f * qd, m8 = -8.0f * qd;
+    const uint32_t qw = qraw[w];
+    const int lo = (int)(qw & 0x0F0F0F0Fu), hi = (int)((qw >> 4) & 0x0F0F0F0Fu);
+    const f32x2 nl01 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, false), nh01 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, false);
+    const f32x2 nl23 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, true), nh23 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, true);
+    // (the empty asm keeps each value an f32 before its conversion: fused into v_fma_mix_f16 the
+    // two roundings would become one, which differs in rare double-rounding cases)
+    float f[8] = {__builtin_fmaf(nl01.x, d512, m8), __builtin_fmaf(nh01.x, d512, m8),
+                  __builtin_fmaf(nl01.y, d512, m8), __builtin_fmaf(nh01.y, d512, m8),
+                  __builtin_fmaf(nl23.x, d512, m8), __builtin_fmaf(nh23.x, d512, m8),
+                  __builtin_fmaf(nl23.y, d512, m8), __builtin_fmaf(nh23.y, d512, m8)};
+    half8 h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      asm volatile("" : "+v"(f[e]));
+      h[e] = (_Float16)f[e];
+    }
+    const int row = ut * T32 + ur;
+    *(half8 *)(g2lds + buf * NPC * G2_PIECE + row * G2_BK + 8 * ((4 * ub + w) ^ (row & 7))) = h;
   };
   f32x4 acc[MR][4];
 #pragma unroll
@@ -290,7 +350,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   const int fr = lane & 15, fk = lane >> 4;
   auto rd = [&](const _Float16 *base, int row, int kk) {  // fragment: 8 halves of `row` at k 8*fk + 32*kk
     const int c = kk * 4 + fk;
-    return *(const half8 *)(base + row * G2_BK + 8 * (c ^ ((row >> 1) & 7)));
+    return *(const half8 *)(base + row * G2_BK + 8 * (c ^ (row & 7)));
   };
   auto rdA = [&](int buf, int mh) {  // rows of the tile: wave half wr, quarter mh
     const _Float16 *bp = g2lds + buf * NPC * G2_PIECE;
@@ -324,31 +384,63 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
   mma(MH, NH, BB);                                     \
   __builtin_amdgcn_sched_barrier(0);
-  // prologue: tile 0 whole, tile 1's B pieces in flight (as if staged in P4 of tile -1)
+  // prologue: tile 0 whole, tile 1's B pieces in flight (as if staged in P4 of tile -1); Q4A:
+  // tile 0's A dequantized, tile 1's raw blocks in registers
 #pragma unroll
   for (int p = AP; p < NPC; ++p) stage(0, p);
+  if constexpr (Q4A) {
+    qload(0, qraw, qd);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);  // the dequant reads the loaded registers after the wait
+    qstore(0);
+    qload(1, qraw_n, qd_n);
+  } else {
 #pragma unroll
-  for (int p = 0; p < AP; ++p) stage(0, p);
+    for (int p = 0; p < AP; ++p) stage(0, p);
+  }
 #pragma unroll
   for (int p = AP; p < NPC; ++p) stage(1, p);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if constexpr (Q4A) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile 0's A stores
   __builtin_amdgcn_s_barrier();
   if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   for (int t = 0; t < nk; ++t) {
     const int cb = t & 1;
     rdA(cb, 0);
     rdB(b0, cb, 0);
+    if constexpr (Q4A) {
+      // tile t+1's A from the raw blocks (waited at the end of P3 of tile t-1), dequantized in
+      // P2 (the phase with the fewest LDS reads) into buffer cb^1: writable from P1 on (its last
+      // reads were P3 of tile t-1), the writes complete by the lgkmcnt(0) ending P3, before
+      // either wave group's first read of it in P1 of tile t+1
+      qraw = qraw_n;
+      qd = qd_n;
+      qload(t + 2, qraw_n, qd_n);  // retired by the vmcnt(0) ending P3, used in P1 of tile t+1
+      G2_SYNC_MMA(0, 0, b0)
+    } else {
 #pragma unroll
-    for (int p = 0; p < AP / 2; ++p) stage(t + 1, p);
-    G2_SYNC_MMA(0, 0, b0)
+      for (int p = 0; p < AP / 2; ++p) stage(t + 1, p);
+      G2_SYNC_MMA(0, 0, b0)
+    }
     __builtin_amdgcn_s_barrier();
     rdB(b1, cb, 1);
+    if constexpr (Q4A) {
 #pragma unroll
-    for (int p = AP / 2; p < AP; ++p) stage(t + 1, p);
-    G2_SYNC_MMA(0, 1, b1)
+      for (int w = 0; w < 4; ++w) qstore_word(cb ^ 1, w);  // (P2 reads the least: 4 B fragments)
+      G2_SYNC_MMA(0, 1, b1)
+    } else {
+#pragma unroll
+      for (int p = AP / 2; p < AP; ++p) stage(t + 1, p);
+      G2_SYNC_MMA(0, 1, b1)
+    }
     __builtin_amdgcn_s_barrier();
     rdA(cb, 1);
-    G2_SYNC_MMA(1, 1, b1)
+    if constexpr (Q4A) {
+      G2_SYNC_MMA(1, 1, b1)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's A writes of tile t+1 landed
+    } else {
+      G2_SYNC_MMA(1, 1, b1)
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B pieces) landed
     __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -547,22 +639,22 @@ static int g2_ap(int M, int n) {
   return cost(3) < cost(4) ? 3 : 4;
 }
 
-template <int AP>
-static int g2_launch(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
+template <int AP, bool Q4A>
+static int g2_launch(const void *A16, const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y,
                      hipStream_t s, const uint16_t *tab, void *q16, const G2Epi &epi) {
   static bool attr = false;
   if (!attr) {
-    const void *fns[] = {(const void *)k_gemm_f16_256<false, AP, 0>, (const void *)k_gemm_f16_256<false, AP, 1>,
-                         (const void *)k_gemm_f16_256<false, AP, 2>, (const void *)k_gemm_f16_256<false, AP, 3>,
-                         (const void *)k_gemm_f16_256<true, AP, 0>};
+    const void *fns[] = {(const void *)k_gemm_f16_256<false, AP, 0, Q4A>, (const void *)k_gemm_f16_256<false, AP, 1, Q4A>,
+                         (const void *)k_gemm_f16_256<false, AP, 2, Q4A>, (const void *)k_gemm_f16_256<false, AP, 3, Q4A>,
+                         (const void *)k_gemm_f16_256<true, AP, 0, Q4A>};
     for (const void *f : fns)
       VSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, g2_lds_bytes(AP)));
     attr = true;
   }
   const int nwg = ((M + 64 * AP - 1) / (64 * AP)) * ((n + G2_BN - 1) / G2_BN);
 #define G2_GO(GQ, EM, TAB, Q)                                                                              \
-  hipLaunchKernelGGL((k_gemm_f16_256<GQ, AP, EM>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s,     \
-                     (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, TAB, (_Float16 *)Q, epi)
+  hipLaunchKernelGGL((k_gemm_f16_256<GQ, AP, EM, Q4A>), dim3(nwg), dim3(G2_THREADS), g2_lds_bytes(AP), s, \
+                     (const _Float16 *)A16, M, K, (const _Float16 *)x16, n, bias, y, TAB, (_Float16 *)Q, epi, WQ)
   if (q16) G2_GO(true, 0, tab, q16);
   else if (epi.cs) G2_GO(false, 1, nullptr, nullptr);
   else if (epi.res) G2_GO(false, 2, nullptr, nullptr);
@@ -573,8 +665,21 @@ static int g2_launch(const void *A16, int M, int K, const void *x16, int n, cons
   return VSIM_OK;
 }
 
+static int g2_checked(const void *A16, const W4 *WQ, int M, int K, const void *x16, int n, const float *bias, float *y,
+                      hipStream_t s, void *q16, const G2Epi *epi);
+
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
                         hipStream_t s, void *q16, const G2Epi *epi) {
+  return g2_checked(A16, nullptr, M, K, x16, n, bias, y, s, q16, epi);
+}
+
+int launch_gemm_q4_256(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s, void *q16,
+                       const G2Epi *epi) {
+  return g2_checked(nullptr, &W, W.rows, W.k, x16, n, bias, y, s, q16, epi);
+}
+
+static int g2_checked(const void *A16, const W4 *WQ, int M, int K, const void *x16, int n, const float *bias, float *y,
+                      hipStream_t s, void *q16, const G2Epi *epi) {
   if (K % G2_BK || K <= 0 || M <= 0 || n <= 0 || (q16 && (M % QK || !bias))) {
     set_error("f16 gemm: K must be a positive multiple of 64 (and M of 32, with a bias, for the GELU epilogue)");
     return VSIM_EINVAL;
@@ -594,8 +699,13 @@ int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, c
     if (int rc = tables_get(&t)) return rc;
     tab = t.gelu_f16;
   }
-  return g2_ap(M, n) == 3 ? g2_launch<3>(A16, M, K, x16, n, bias, y, s, tab, q16, e)
-                          : g2_launch<4>(A16, M, K, x16, n, bias, y, s, tab, q16, e);
+  if (WQ) {
+    return g2_ap(M, n) == 3 ? g2_launch<3, true>(nullptr, *WQ, M, K, x16, n, bias, y, s, tab, q16, e)
+                            : g2_launch<4, true>(nullptr, *WQ, M, K, x16, n, bias, y, s, tab, q16, e);
+  }
+  const W4 none{};
+  return g2_ap(M, n) == 3 ? g2_launch<3, false>(A16, none, M, K, x16, n, bias, y, s, tab, q16, e)
+                          : g2_launch<4, false>(A16, none, M, K, x16, n, bias, y, s, tab, q16, e);
 }
 
 int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool gelu, void *x16, hipStream_t s) {

@@ -112,10 +112,6 @@ struct vsim_model {
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
   float *fast_ffp = nullptr, *fast_part = nullptr;
   void *pf_scratch = nullptr;  // fast prefill: fp16 K / V^T copies (attn_prefill.hip)
-  // fast prefill of long prompts: fp16 images [M][K] of the Q4_0 weights (2 bytes per weight,
-  // made on first use, dropped when a weight changes), for the 256 x 256-tile GEMM
-  std::map<const void *, void *> w16;
-  size_t w16_bytes = 0;
   void *pf_x16 = nullptr;      // fast prefill: fp16 GEMM operands, [n_max][E] then [n_max][4E]
   size_t pf_bytes = 0;
 
@@ -153,12 +149,6 @@ struct vsim_model {
 namespace {
 
 int E_(const vsim_model *m) { return m->hp.n_embd; }
-
-void free_w16(vsim_model *m) {
-  for (auto &kv : m->w16) (void)hipFree(kv.second);
-  m->w16.clear();
-  m->w16_bytes = 0;
-}
 
 void free_scratch(vsim_model *m) {
   void *ps[] = {m->inpL, m->cur1, m->cur2, m->Qb, m->Kb, m->Vb, m->attn_in, m->attn, m->ff, m->fch, m->kq,
@@ -495,33 +485,6 @@ int prof_collect(vsim_model *m) {
 
 double w4_algo_bytes(const W4 &w) { return (double)w.rows * w.k / QK * QBYTES; }
 
-// The fp16 image of a weight for the long-prompt GEMM, made on first use (false: no room for
-// it, and that weight's GEMMs stay on the in-LDS-dequant kernel).
-bool g2_image(vsim_model *m, const void *W, int M, int K, int &nk) {
-  if (m->w16.count(W)) return true;
-  const size_t bytes = (size_t)M * K * sizeof(uint16_t);
-  // budget: images never take the device below W16_HEADROOM free bytes, so scratch growth,
-  // a second model or the caller's own buffers still find room
-  size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + W16_HEADROOM) {
-    (void)hipGetLastError();
-    return false;
-  }
-  void *img = nullptr;
-  if (hipMalloc(&img, bytes) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  if (launch_w4_expand_f16(w4_view(W, M, K), img, m->stream) != VSIM_OK) {
-    (void)hipFree(img);
-    return false;
-  }
-  m->w16[W] = img;  // only once the expand is queued: a failed launch leaves no stale entry
-  m->w16_bytes += bytes;
-  ++nk;
-  return true;
-}
-
 // Quantize an activation and run one GEMV in the model's mode.  x16 non-null (fast-mode
 // prompt batches): the activation is already the GEMM's fp16 operand (launch_act_quant_f16).
 // gq (fc_in of a long prompt): bias gq_bias + GELU + quantize of the product straight into the
@@ -535,13 +498,12 @@ int mm(vsim_model *m, const void *W, int M, int K, const float *x, int N, uint8_
     RC(launch_q4_quantize(x, K, N, xq, xd, m->stream));
     ++nk;
   }
-  // long prompt: the 256-wide-tile GEMM on the weight's fp16 image
-  if (x16 && N >= G2_MIN_N && K % 64 == 0 && g2_image(m, W, M, K, nk)) {
-    void *img = m->w16[W];
+  // long prompt: the 256-wide-tile GEMM, the Q4_0 weight dequantized to fp16 in LDS
+  if (x16 && N >= G2_MIN_N && K % 64 == 0) {
     const bool gelu = gq && gq_bias && M % QK == 0;
     const long ev = prof_begin(m);
-    RC(launch_gemm_f16_256(img, M, K, x16, N, gelu ? gq_bias : bias, y, m->stream, gelu ? gq : nullptr,
-                           gelu ? nullptr : epi));
+    RC(launch_gemm_q4_256(w4_view(W, M, K), x16, N, gelu ? gq_bias : bias, y, m->stream, gelu ? gq : nullptr,
+                          gelu ? nullptr : epi));
     prof_end(m, ev, "k_gemm_f16_256 (prompt)", (double)M * K / QK * QBYTES);
     ++nk;
     if (fused) *fused = gelu || epi;
@@ -643,8 +605,7 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // long GPT-J prompt: RoPE and the KV-cache write (vsim.cpp:553-580) in the Q/K/V GEMMs'
   // epilogues -- K and V straight into their cache rows -- instead of a pass of their own
   const bool g2 = pf && N >= G2_MIN_N && E % 64 == 0;
-  const bool rope_epi = g2 && gptj && g2_image(m, L.wq, E, E, nk) && g2_image(m, L.wk, E, E, nk) &&
-                        g2_image(m, L.wv, E, E, nk);
+  const bool rope_epi = g2 && gptj;
   G2Epi er;
   er.cs = m->rope_cs;
   er.d = d;
@@ -726,7 +687,7 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   G2Epi ej;
   ej.res = m->inpL;
   ej.res_a = serial ? nullptr : m->attn;
-  const bool join_epi = g2 && g2_image(m, L.wproj, E, F, nk);
+  const bool join_epi = g2;
   bool joined = false;
   RC(mm(m, L.wproj, E, F, m->fch, N, m->xq3, m->xd3, true, L.bproj, join_epi ? m->inpL : m->ff, nk, X.b, nullptr,
         nullptr, &joined, join_epi ? &ej : nullptr));
@@ -1294,7 +1255,6 @@ void vsim_model_free(vsim_model *m) {
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   if (m->alibi) (void)hipFree(m->alibi);
   free_scratch(m);
-  free_w16(m);
   if (m->warena) (void)hipFree(m->warena);
   if (m->kcache && !m->borrowed) (void)hipFree(m->kcache);
   if (m->vcache && !m->borrowed) (void)hipFree(m->vcache);
@@ -1306,10 +1266,6 @@ void vsim_model_free(vsim_model *m) {
 
 int vsim_model_set_tensor(vsim_model *m, const char *name, const void *host, size_t nbytes) {
   if (m->borrowed) { set_error("set_tensor: the weights belong to the graph executor"); return VSIM_EINVAL; }
-  if (!m->w16.empty()) {  // fp16 weight images are remade from the new weights on next use
-    (void)hipStreamSynchronize(m->stream);
-    free_w16(m);
-  }
   {  // BLOOM's fused query_key_value weight: three [E][E] row blocks, q | k | v
     const std::string n(name), suf = "attention.query_key_value.weight";
     if (m->arch == VSIM_ARCH_BLOOM && n.size() >= suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0) {
@@ -1374,10 +1330,6 @@ int vsim_model_get_tensor(vsim_model *m, const char *name, void *host, size_t nb
 int vsim_model_randomize(vsim_model *m, uint64_t seed, float stddev) {
   if (m->borrowed) { set_error("randomize: the weights belong to the graph executor"); return VSIM_EINVAL; }
   VSIM_HIP(hipSetDevice(m->device));
-  if (!m->w16.empty()) {
-    VSIM_HIP(hipStreamSynchronize(m->stream));
-    free_w16(m);
-  }
   uint64_t id = 0;
   for (auto &kv : m->slots) {
     Slot &s = kv.second;

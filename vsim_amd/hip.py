@@ -30,7 +30,7 @@ EXPORTS = [
     "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_act_repack", "vsim_op_act_unpack",
     "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_q4_expand_f16", "vsim_op_gemm_f16",
     "vsim_op_act_quant_f16", "vsim_op_gemm_f16_gelu_q", "vsim_op_gemm_f16_rope", "vsim_op_gemm_f16_join",
-    "vsim_op_get_rows",
+    "vsim_op_gemm_q4_256", "vsim_op_get_rows",
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
     "vsim_op_attn_prefill",
     "vsim_op_tables",
@@ -41,7 +41,7 @@ EXPORTS = [
     "vsim_model_logits_dev", "vsim_model_info", "vsim_model_set_graph", "vsim_model_set_profile",
     "vsim_model_profile_kernel", "vsim_model_profile_stats", "vsim_model_free",
     "vsim_graph_compute", "vsim_graph_compute_rc", "vsim_graph_sync_tensor", "vsim_graph_reset", "vsim_graph_stats",
-    "vsim_graph_set_profile", "vsim_graph_profile_report",
+    "vsim_graph_set_profile", "vsim_graph_profile_report", "vsim_graph_match", "vsim_graph_fast_stats",
     "vsim_model_stage_bind", "vsim_model_stage_begin", "vsim_model_stage_step", "vsim_model_sync",
     "vsim_model_debug_poison",
 ]
@@ -120,6 +120,7 @@ def lib():
     L.vsim_op_gemm_f16_gelu_q.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp]
     L.vsim_op_gemm_f16_rope.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp, ci, ci, ci, vp]
     L.vsim_op_gemm_f16_join.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp, vp]
+    L.vsim_op_gemm_q4_256.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp]
     L.vsim_op_norm.argtypes = [vp, vp, ci, ci, vp, vp, vp]
     L.vsim_op_gelu.argtypes = [vp, vp, ci, vp]
     L.vsim_op_attn_softmax.argtypes = [vp, ci, ci, ci, ci, cf, vp]
