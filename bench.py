@@ -108,6 +108,27 @@ def roofline_from_profile(kernels, wall_s, mode):
     }
 
 
+def measured_copy_gbps(nbytes=2 << 30, reps=10):
+    """Device-to-device copy bandwidth on this GPU (a measured figure beside the
+    8 TB/s spec): torch's copy of a 2 GiB buffer, read + write bytes / time, best of reps."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    best = 0.0
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        best = max(best, 2.0 * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del a, b
+    return round(best, 1)
+
+
 def metric_name(config: str) -> str:
     """BASELINE.json's metric for the headline config; the same wording for the others."""
     if config == "gpt-j-6B":
@@ -117,18 +138,6 @@ def metric_name(config: str) -> str:
 
 def q4_weight_bytes(arch: str, hp: mg.HParams) -> float:
     """B_w per decode token: every Q4_0 matrix incl. lm_head, 0.625 B/w."""
-    exact = None
-    if args.prefill_exact:
-        model.set_mode(hip.MODE_EXACT)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        model.eval(0, ids)
-        torch.cuda.synchronize()
-        te = time.perf_counter() - t0
-        model.set_mode(hip.MODE_FAST)
-        exact = {"ms_per_prompt": round(te * 1e3, 1), "value": round(N / te, 1), "unit": "tokens/s",
-                 "path": "exact mode: per-token fp32 chains (the reference's sumf order), bit-identical to the oracle",
-                 "steps": 1}
     E, F, L, V = hp.n_embd, hp.n_ff, hp.n_layer, hp.n_vocab
     return 0.625 * (L * (4 * E * E + 2 * E * F) + V * E)
 
@@ -397,6 +406,18 @@ def run_prefill(args, dev):
         model.eval(0, ids)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
+    exact = None
+    if args.prefill_exact:
+        model.set_mode(hip.MODE_EXACT)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        model.eval(0, ids)
+        torch.cuda.synchronize()
+        te = time.perf_counter() - t0
+        model.set_mode(hip.MODE_FAST)
+        exact = {"ms_per_prompt": round(te * 1e3, 1), "value": round(N / te, 1), "unit": "tokens/s",
+                 "path": "exact mode: per-token fp32 chains (the reference's sumf order), bit-identical to the oracle",
+                 "steps": 1}
     E, F, L, V = hp.n_embd, hp.n_ff, hp.n_layer, hp.n_vocab
     # flops as computed: every layer matmul over N tokens, the head for the last row (the
     # logits that leave the eval, vsim.cpp:736-737), causal QK^T and PV
@@ -518,6 +539,9 @@ def main():
         kernels = model.profile_kernels()
         model.set_profile(False)
         roofline = roofline_from_profile(kernels, prof_wall, args.mode)
+        if roofline is not None:
+            roofline["measured_copy_GBps"] = measured_copy_gbps()
+            roofline["frac_of_measured_copy"] = round(roofline["achieved"] / roofline["measured_copy_GBps"], 4)
 
     tokens_total = args.steps * world
     value = tokens_total / elapsed

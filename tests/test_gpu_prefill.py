@@ -23,8 +23,13 @@ from vsim_amd import modelgen as mg
 pytestmark = pytest.mark.gpu
 
 NTH = max(1, min(16, os.cpu_count() or 1))
-# fast prompt vs the reference's exact composition: logits direction and greedy token
-FAST_COS_MIN = 0.97  # measured r02: 0.976-0.996 over 12 prompts of the small models
+# fast prompt vs the reference's exact composition: the bounds are set once from the recorded
+# distribution profiles/r03_fast_prefill_e2e_distribution.json (tools/fast_prefill_distribution.py:
+# 72 prompts of these three models at N = 72 and 288, other prompts than the ones below):
+# cos min 0.9741, 5th percentile 0.9771, median 0.9884; the fast greedy token within the oracle's
+# top 5 in 72 of 72, equal to the oracle's in 49 of 72 (so no per-prompt top-1 bound).  The
+# cos bound is the recorded minimum less a margin of 0.014; neither is edited after a red run.
+FAST_COS_MIN = 0.96
 
 
 def bits(a):
@@ -82,12 +87,9 @@ def test_fast_prompt_vs_oracle(cfg, N, tmp_path):
     msg = f"{cfg}: cos {['%.5f' % c for c in cos]}, max-rel {['%.3g' % r[1] for r in res]}, top-1 {top1}/4"
     print(msg)
     assert min(cos) >= FAST_COS_MIN, msg
-    # the greedy token: the random parity models' top logits are close, and at N = 288 the
-    # re-quantization flips of fast mode move them past each other on either GEMM (r02 A/B:
-    # top-1 2-4/4 with the 128-tile in-LDS-dequant GEMM as with the 256-tile one), so there the
-    # bound is the oracle's top 5
-    if N <= 72:
-        assert top1 >= 3, msg
+    # the greedy token: the random parity models' top logits are close and the re-quantization
+    # flips of fast mode move them past each other (top-1 49/72 recorded), so the bound is the
+    # oracle's top 5 (72/72 recorded)
     assert all(r[3] for r in res), msg
 
 
