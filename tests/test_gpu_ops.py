@@ -229,10 +229,23 @@ def test_gemv_exact_full_width_vs_oracle(M, K):
     assert np.array_equal(bits(gemv(w, M, K, xq, xd, 1, hip.MODE_EXACT)), bits(ref))
 
 
+
+def w16_of(w_aos, K):
+    """The fp16 weight operand of the prompt GEMMs: each Q4_0 value d*(q-8) rounded ONCE to
+    fp16 from its exact value (gemm_f16.hip deq_word_f16: one v_fma_mix; the product d*(q-8)
+    is exact in fp64 and numpy's fp64 -> fp16 conversion rounds to nearest even directly)."""
+    blk = np.asarray(w_aos, dtype=np.uint8).reshape(-1, mg.QBYTES)
+    d = blk[:, :4].copy().view(np.float32).reshape(-1).astype(np.float64)
+    q = np.empty((blk.shape[0], 32), dtype=np.float64)
+    q[:, 0::2] = (blk[:, 4:] & 0xF).astype(np.float64) - 8
+    q[:, 1::2] = (blk[:, 4:] >> 4).astype(np.float64) - 8
+    return (q * d[:, None]).astype(np.float16).reshape(-1, K)
+
 @pytest.mark.parametrize("M,K,N", [(520, 512, 300), (256, 4096, 8), (1000, 1024, 129), (96, 96, 40)])
 def test_prefill_gemm_f16(M, K, N):
     """Fast-mode prompt GEMM (gemm_f16.hip: fp16 MFMA after in-LDS dequant).  Operands are
-    d*(q-8) rounded once to fp16, products exact, fp32 accumulation: the result must be
+    d*(q-8) rounded to fp16 (the weight once from its exact value, w16_of; the activation via
+    its f32 value), products exact, fp32 accumulation: the result must be
     within 4*K*2^-24*sum|w16*x16| of the fp64 product of the fp16-rounded operands, and
     within 2^-10*sum|w*x| (operand rounding) of the unrounded Q4_0 x Q4_0 product.
     Ragged M and N (not multiples of the 128 x 128 tile) and K = 96 (odd block count)."""
@@ -246,7 +259,7 @@ def test_prefill_gemm_f16(M, K, N):
     hip.check(hip.lib().vsim_op_act_unpack(xq.data_ptr(), xq_aos.data_ptr(), N, K, None), "unpack")
     W = mg.dequantize_q4_0(w_aos, K)
     X = mg.dequantize_q4_0(host(xq_aos), K)
-    W16 = W.astype(np.float16).astype(np.float64)
+    W16 = w16_of(w_aos, K).astype(np.float64)
     X16 = X.astype(np.float16).astype(np.float64)
     ref16 = X16 @ W16.T + b
     abs16 = np.abs(X16) @ np.abs(W16).T
@@ -301,7 +314,7 @@ def test_prompt_gemm_vs_reference_mul_mat(c):
                                    (300, 4096, 257), (24576, 64, 2048)])
 def test_prefill_gemm_f16_256(M, K, N):
     """Long-prompt GEMM (gemm_f16.hip k_gemm_f16_256 on the fp16 weight image of
-    k_w4_expand_f16): the image holds exactly the fp16 roundings of d*(q-8); the product is
+    k_w4_expand_f16): the image holds exactly the fp16 roundings of d*(q-8) (w16_of); the product is
     within 4*K*2^-24*sum|w16*x16| of the fp64 product of the same fp16 operands.  Ragged M
     and N (not multiples of the tile), K = 64 and 128 (one and two K-tiles: the prologue's and
     loop's clamped stages), K = 4096; 192-row tiles everywhere but (24576, 64, 2048), whose
@@ -310,7 +323,7 @@ def test_prefill_gemm_f16_256(M, K, N):
     w_aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05))
     b = rng.standard_normal(M).astype(np.float32)
     w = repack(w_aos, M, K)
-    W16 = mg.dequantize_q4_0(w_aos, K).astype(np.float16)
+    W16 = w16_of(w_aos, K)
     img = torch.empty(M * K, dtype=torch.float16, device=DEV)
     hip.check(hip.lib().vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
     torch.cuda.synchronize()

@@ -29,41 +29,59 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int GM_BM = 128, GM_BN = 128, GM_BK = 64, GM_THREADS = 256;
 constexpr int GM_LD = GM_BK + 8;  // halves per LDS row: 16-byte pad against bank conflicts
 
-// 32 fp16 values d * (q - 8) of one Q4_0 block (byte j: element 2j low nibble, 2j+1 high)
-__device__ __forceinline__ void deq_block_f16(uint4 q, float d, half8 out[4]) {
-  const f32x2 d2 = {512.0f * d, 512.0f * d}, m2 = {-8.0f * d, -8.0f * d};
-  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const int lo = (int)(qw[w] & 0x0F0F0F0Fu), hi = (int)((qw[w] >> 4) & 0x0F0F0F0Fu);
-    // elements 8w .. 8w+7: (lo b0, hi b0, lo b1, hi b1, lo b2, hi b2, lo b3, hi b3)
-    const f32x2 l01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, false), d2, m2);
-    const f32x2 h01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, false), d2, m2);
-    const f32x2 l23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, true), d2, m2);
-    const f32x2 h23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, true), d2, m2);
-    half8 h;
-    h[0] = (_Float16)l01.x;
-    h[1] = (_Float16)h01.x;
-    h[2] = (_Float16)l01.y;
-    h[3] = (_Float16)h01.y;
-    h[4] = (_Float16)l23.x;
-    h[5] = (_Float16)h23.x;
-    h[6] = (_Float16)l23.y;
-    h[7] = (_Float16)h23.y;
-    out[w] = h;
-  }
+// 8 fp16 values d * (q - 8) of one word of a Q4_0 block (elements 8w .. 8w+7: lo b0, hi b0,
+// lo b1, hi b1, ...): the nibble n as n 2^-9 from the fp8 conversion, then one fused multiply-add
+// that rounds the exact d (n - 8) once, straight to fp16 (v_fma_mix_f16; the file is built
+// without SLP vectorization so the scalar FMAs are not re-packed into v_pk_fma_f32 + a separate
+// conversion, which would round twice).  Every fp16 weight operand of the prompt GEMMs comes
+// from here: the fp16 image (k_w4_expand_f16), the in-LDS dequant, the 128-tile kernel.
+__device__ __forceinline__ half8 deq_word_f16(uint32_t qw, float d) {
+  const float d512 = 512.0f * d, m8 = -8.0f * d;
+  const int lo = (int)(qw & 0x0F0F0F0Fu), hi = (int)((qw >> 4) & 0x0F0F0F0Fu);
+  const f32x2 nl01 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, false), nh01 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, false);
+  const f32x2 nl23 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, true), nh23 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, true);
+  half8 h;
+  h[0] = (_Float16)__builtin_fmaf(nl01.x, d512, m8);
+  h[1] = (_Float16)__builtin_fmaf(nh01.x, d512, m8);
+  h[2] = (_Float16)__builtin_fmaf(nl01.y, d512, m8);
+  h[3] = (_Float16)__builtin_fmaf(nh01.y, d512, m8);
+  h[4] = (_Float16)__builtin_fmaf(nl23.x, d512, m8);
+  h[5] = (_Float16)__builtin_fmaf(nh23.x, d512, m8);
+  h[6] = (_Float16)__builtin_fmaf(nl23.y, d512, m8);
+  h[7] = (_Float16)__builtin_fmaf(nh23.y, d512, m8);
+  return h;
 }
 
-// The activation rows dequantized once per GEMM call (the same halves the in-GEMM dequant
-// produced): X16[token][K], block i = token * nb + b at X16 + 32 i.
+// 32 fp16 values d * (q - 8) of one Q4_0 block (byte j: element 2j low nibble, 2j+1 high)
+__device__ __forceinline__ void deq_block_f16(uint4 q, float d, half8 out[4]) {
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) out[w] = deq_word_f16(qw[w], d);
+}
+
+// The activation rows dequantized once per GEMM call: X16[token][K], block i = token * nb + b
+// at X16 + 32 i, each value (fp16)(d * (q - 8)) with the f32 product rounded first -- the
+// halves k_act_quant_f16 writes (activations round twice, the weights once: deq_word_f16).
 __global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__ xqs, const float *__restrict__ xdd,
                                                       size_t nblk, half8 *__restrict__ X16) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nblk) return;
-  half8 h[4];
-  deq_block_f16(*(const uint4 *)(xqs + i * 16), xdd[i], h);
+  const uint4 q = *(const uint4 *)(xqs + i * 16);
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+  const float d = xdd[i];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) X16[4 * i + w] = h[w];
+  for (int w = 0; w < 4; ++w) {
+    half8 h;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float p0 = d * (float)((int)((qw[w] >> (8 * j)) & 15u) - 8);
+      float p1 = d * (float)((int)((qw[w] >> (8 * j + 4)) & 15u) - 8);
+      asm volatile("" : "+v"(p0), "+v"(p1));  // (kept apart from the conversion: two roundings)
+      h[2 * j] = (_Float16)p0;
+      h[2 * j + 1] = (_Float16)p1;
+    }
+    X16[4 * i + w] = h;
+  }
 }
 
 // Prompt activation rows straight to the GEMM's fp16 operand: (bias + GELU table,
@@ -255,8 +273,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Q4A: the weight operand is the W4T32 Q4_0 weight WQ itself (0.625 B per weight from HBM, no
 // fp16 image): each K-tile's raw blocks are loaded into registers in P2 two tiles ahead (one
 // Q4_0 block of one row per thread: 16 nibble bytes + the scale, a wave = one 32-row tile's two
-// blocks, 1 KB + 256 B contiguous) and in P1 of the tile before their use dequantized with
-// deq_block_f16 -- the same fp16 halves k_w4_expand_f16 writes -- into the A pieces of the LDS
+// blocks, 1 KB + 256 B contiguous) and in P2 of the tile before their use dequantized with
+// deq_word_f16 -- the same fp16 halves k_w4_expand_f16 writes -- into the A pieces of the LDS
 // buffer, where the DMA of the image path would have put them (same swizzle, same reads).
 template <bool GQ, int AP, int EM, bool Q4A = false>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
@@ -315,29 +333,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
 #pragma unroll
     for (int j = 0; j < 4; ++j) *(half8 *)(base + 8 * ((4 * ub + j) ^ (row & 7))) = h[j];
   };
-  // one word (8 values) of the unit: deq_block_f16's arithmetic for word w, stored to its chunk
-  // (scalar v_fma_f32, not the packed form deq_block_f16 uses: beside MFMAs a v_pk_fma_f32
-  // costs ~22 cycles more than two v_fma_f32, MI355X_MICROARCH.md; same values: fma(n 2^-9,
-  // 512 d, -8 d) rounds d (n - 8) once, then once more to fp16)
+  // one word (8 values) of the unit, stored to its chunk
   auto qstore_word = [&](int buf, int w) {
     if (!qown) return;
-    const float d512 = 512.0f * qd, m8 = -8.0f * qd;
-    const uint32_t qw = qraw[w];
-    const int lo = (int)(qw & 0x0F0F0F0Fu), hi = (int)((qw >> 4) & 0x0F0F0F0Fu);
-    const f32x2 nl01 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, false), nh01 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, false);
-    const f32x2 nl23 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, true), nh23 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, true);
-    // (the empty asm keeps each value an f32 before its conversion: fused into v_fma_mix_f16 the
-    // two roundings would become one, which differs in rare double-rounding cases)
-    float f[8] = {__builtin_fmaf(nl01.x, d512, m8), __builtin_fmaf(nh01.x, d512, m8),
-                  __builtin_fmaf(nl01.y, d512, m8), __builtin_fmaf(nh01.y, d512, m8),
-                  __builtin_fmaf(nl23.x, d512, m8), __builtin_fmaf(nh23.x, d512, m8),
-                  __builtin_fmaf(nl23.y, d512, m8), __builtin_fmaf(nh23.y, d512, m8)};
-    half8 h;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      asm volatile("" : "+v"(f[e]));
-      h[e] = (_Float16)f[e];
-    }
+    const half8 h = deq_word_f16(qraw[w], qd);
     const int row = ut * T32 + ur;
     *(half8 *)(g2lds + buf * NPC * G2_PIECE + row * G2_BK + 8 * ((4 * ub + w) ^ (row & 7))) = h;
   };
