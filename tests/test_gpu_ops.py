@@ -213,10 +213,13 @@ def rand_q4_aos(rng, M, K, std=0.02):
 
 
 # Shapes and the kernel launch_gemv_chain_batch picks for them (gemv_chain.hip): >= 192
-# 64-row groups -> k_gemv_solo (the bench's Q/K/V + fc_in batch, 28672 x 4096, and the heads),
-# fewer -> k_gemv_chain32 (fc_out, out-projection).
+# 128-row groups -> k_gemv_solo with two consumers (the bench's Q/K/V + fc_in batch, 28672 x
+# 4096; 24600 x 4096: a ragged last group and a partial last tile; the heads), else >= 192
+# 64-row groups -> k_gemv_solo with one (fc_in alone, 16384 x 4096), fewer -> k_gemv_chain32
+# (fc_out, out-projection).
 @pytest.mark.parametrize("M,K", [(4096, 4096), (1024, 16384), (50400, 256), (16384, 4096), (28672, 4096),
-                                 (50400, 4096), (50432, 6144), (250880, 1024), (6144, 24576), (4064, 4096)])
+                                 (24600, 4096), (50400, 4096), (50432, 6144), (250880, 1024), (6144, 24576),
+                                 (4064, 4096)])
 def test_gemv_exact_full_width_vs_oracle(M, K):
     """GPT-J / 20B / BLOOM widths (K = n_embd and 4*n_embd, V rows) against the CPU restatement."""
     import oracle_py as O

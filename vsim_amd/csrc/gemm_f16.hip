@@ -276,6 +276,180 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // blocks, 1 KB + 256 B contiguous) and in P2 of the tile before their use dequantized with
 // deq_word_f16 -- the same fp16 halves k_w4_expand_f16 writes -- into the A pieces of the LDS
 // buffer, where the DMA of the image path would have put them (same swizzle, same reads).
+// The epilogue of one wave's region of the prompt GEMM: MW rows from mw x 64 columns from nc0,
+// acc in the 16x16 MFMA C/D map (column (token) = lane & 15, rows 4 * (lane >> 4) + reg of each
+// 16 x 16 fragment).  GQ: bias + GELU + quantize into Q16 (fp16); else the f32 tile Y through
+// this wave's LDS area (LDSB: the workgroup's LDS bytes, 8 waves), with the EM extra work.
+// The caller has passed a barrier after its last LDS operand read; a wave may call it again
+// for its next region (its own LDS writes and reads are ordered).
+template <bool GQ, int EM, int MW, int LDSB>
+__device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int mw, int nc0, int M, int N,
+                                            const float *__restrict__ bias, float *__restrict__ Y,
+                                            const uint16_t *__restrict__ gelu_tab, _Float16 *__restrict__ Q16,
+                                            const G2Epi &epi, _Float16 *lds, int wave, int lane) {
+  const int fr = lane & 15, fk = lane >> 4;
+  if constexpr (GQ) {
+    // quantized fp16 values go through LDS too (as the f32 tile below): direct stores would
+    // write 32-byte pieces of 16 columns per instruction
+    constexpr int LDH = MW + 8;  // LDS row stride (halves, padded)
+    _Float16 *eh = lds + wave * 32 * LDH;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int p = 0; p < MW / 32; ++p) {
+      const int mb = mw + 32 * p;  // the block's first row
+      float bv[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bv[e] = mb + 4 * fk + e < M ? bias[mb + 4 * fk + e] : 0.0f;
+        bv[4 + e] = mb + 16 + 4 * fk + e < M ? bias[mb + 16 + 4 * fk + e] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 2 * pass; j < 2 * pass + 2; ++j) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = h2f(gelu_tab[f2h(acc[2 * p][j][e] + bv[e])]);
+          v[4 + e] = h2f(gelu_tab[f2h(acc[2 * p + 1][j][e] + bv[4 + e])]);
+        }
+        float amax = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = amax > fabsf(v[e]) ? amax : fabsf(v[e]);
+        float o = __shfl_xor(amax, 16, 64);
+        amax = amax > o ? amax : o;
+        o = __shfl_xor(amax, 32, 64);
+        amax = amax > o ? amax : o;
+        const float d = amax / 7.0f;
+        const float id = d != 0.0f ? 1.0f / d : 0.0f;
+        _Float16 h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (_Float16)(d * (float)(x86_round_i8(v[e] * id)));
+        _Float16 *row = eh + ((j & 1) * 16 + fr) * LDH + 32 * p + 4 * fk;
+        *(uint2 *)row = *(const uint2 *)&h[0];
+        *(uint2 *)(row + 16) = *(const uint2 *)&h[4];
+      }
+    }
+    // (M % 32 == 0: a chunk of 8 rows is wholly in or out)
+    for (int idx = lane; idx < 32 * (MW / 8); idx += 64) {
+      const int nl = idx / (MW / 8), c = idx % (MW / 8);
+      const int n = nc0 + 32 * pass + nl, m = mw + 8 * c;
+      const uint4 v = *(const uint4 *)(eh + nl * LDH + 8 * c);
+      if (n < N && m < M) *(uint4 *)(Q16 + (size_t)n * M + m) = v;
+    }
+    }
+    return;
+  }
+  // The f32 tile leaves through LDS: a lane's accumulator holds 4 consecutive rows m of one
+  // column n, so direct stores write 16 columns x 64 bytes per instruction; each wave instead
+  // writes its (BM/2) x 64 region into its own LDS area, CP columns at a time, and stores
+  // whole runs of (BM/2) floats per column (the direct stores cost 8-10 % of the GEMM).
+  constexpr int LDW = MW + 4;  // LDS row stride (floats, padded)
+  constexpr int CP = 8 * 32 * LDW * 4 <= LDSB ? 32 : 16;  // columns per pass
+  float *ep = (float *)lds + wave * CP * LDW;
+  const bool vec = (M & 3) == 0;
+#pragma unroll
+  for (int pass = 0; pass < 64 / CP; ++pass) {
+#pragma unroll
+    for (int i = 0; i < MW / 16; ++i)
+#pragma unroll
+      for (int jj = 0; jj < CP / 16; ++jj)
+        *(f32x4 *)(ep + (16 * jj + fr) * LDW + 16 * i + 4 * fk) = acc[i][(CP / 16) * pass + jj];
+    // (a wave's own LDS writes and reads are ordered)
+    constexpr int RW = MW / 4, NIT = CP * RW / 64;  // float4 chunks per column run; per lane
+    static_assert(CP * RW % 64 == 0, "whole chunks per lane");
+    // the epilogue's extra inputs, all loaded before the pass's first store (Y may be epi.res,
+    // and a load behind a store it may alias waits for it: one exposed latency per chunk)
+    [[maybe_unused]] f32x4 xr[EM == 2 ? NIT : 1], xa[EM == 2 ? NIT : 1];
+    [[maybe_unused]] double2 cq[EM == 1 ? NIT : 1][2];
+    if constexpr (EM != 0) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
+        const int n = nc0 + CP * pass + nl, m = mw + 4 * c;
+        if (n >= N || m >= M) continue;
+        if constexpr (EM == 2) {
+          xr[it] = *(const f32x4 *)(epi.res + (size_t)n * M + m);
+          if (epi.res_a) xa[it] = *(const f32x4 *)(epi.res_a + (size_t)n * M + m);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int dd = (m + 2 * q) % epi.d;
+            cq[it][q] = dd < epi.n_rot ? epi.cs[(size_t)(epi.p0 + n) * (epi.n_rot / 2) + dd / 2] : make_double2(1.0, 0.0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
+      const int n = nc0 + CP * pass + nl, m = mw + 4 * c;
+      f32x4 v = *(const f32x4 *)(ep + nl * LDW + 4 * c);
+      if (n >= N || m >= M) continue;
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += m + e < M ? bias[m + e] : 0.0f;
+      }
+      if constexpr (EM == 1) {  // (the launcher guarantees M % 4 == 0 and an even d: pairs stay in the run)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if ((m + 2 * q) % epi.d < epi.n_rot) {
+            const double2 cs = cq[it][q];
+            const double x0 = v[2 * q], x1 = v[2 * q + 1];
+            v[2 * q] = (float)(x0 * cs.x - x1 * cs.y);
+            v[2 * q + 1] = (float)(x0 * cs.y + x1 * cs.x);
+          }
+        }
+        if (epi.h16) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          *(h4 *)(epi.h16 + (size_t)(epi.p0 + n) * M + m) = (h4){(_Float16)v[0], (_Float16)v[1], (_Float16)v[2],
+                                                                 (_Float16)v[3]};
+        }
+      }
+      if constexpr (EM == 2) {
+        if (epi.res_a) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = xr[it][e] + (xa[it][e] + v[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] + xr[it][e];
+        }
+      }
+      float *dst = Y + (size_t)n * M + m;
+      if (vec && m + 3 < M) {
+        *(f32x4 *)dst = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (m + e < M) dst[e] = v[e];
+      }
+    }
+    if constexpr (EM == 3) {
+      // the pass's columns again, read down the LDS region: runs of 8 columns of one row m,
+      // as fp16, into row m of the transposed copy (4 lanes cover a row's 32 columns)
+      constexpr int C8 = CP / 8, NT2 = MW * C8 / 64;
+      static_assert(MW * C8 % 64 == 0, "whole runs per lane");
+#pragma unroll
+      for (int it = 0; it < NT2; ++it) {
+        const int idx = lane + 64 * it, c8 = idx % C8, ml = idx / C8;
+        const int m = mw + ml, nb = nc0 + CP * pass + 8 * c8;
+        if (m >= M || nb >= N) continue;
+        const float bm = bias ? bias[m] : 0.0f;
+        half8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (_Float16)(ep[(8 * c8 + j) * LDW + ml] + bm);
+        _Float16 *dst = epi.h16 + (size_t)m * epi.h16_ld + epi.p0 + nb;
+        if (nb + 8 <= N && ((epi.p0 + nb) & 7) == 0) {
+          *(half8 *)dst = h;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (nb + j < N) dst[j] = h[j];
+        }
+      }
+    }
+  }
+}
+
 template <bool GQ, int AP, int EM, bool Q4A = false>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *__restrict__ A, int M, int K,
                                                                  const _Float16 *__restrict__ B, int N,
@@ -392,14 +566,14 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);  // the dequant reads the loaded registers after the wait
     qstore(0);
-    qload(1, qraw_n, qd_n);
+    qload(1, qraw_n, qd_n);  // waited in P2 of tile 0
   } else {
 #pragma unroll
     for (int p = 0; p < AP; ++p) stage(0, p);
   }
 #pragma unroll
   for (int p = AP; p < NPC; ++p) stage(1, p);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed (Q4A: and tile 1's raw blocks)
   if constexpr (Q4A) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile 0's A stores
   __builtin_amdgcn_s_barrier();
   if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
@@ -408,13 +582,6 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     rdA(cb, 0);
     rdB(b0, cb, 0);
     if constexpr (Q4A) {
-      // tile t+1's A from the raw blocks (waited at the end of P3 of tile t-1), dequantized in
-      // P2 (the phase with the fewest LDS reads) into buffer cb^1: writable from P1 on (its last
-      // reads were P3 of tile t-1), the writes complete by the lgkmcnt(0) ending P3, before
-      // either wave group's first read of it in P1 of tile t+1
-      qraw = qraw_n;
-      qd = qd_n;
-      qload(t + 2, qraw_n, qd_n);  // retired by the vmcnt(0) ending P3, used in P1 of tile t+1
       G2_SYNC_MMA(0, 0, b0)
     } else {
 #pragma unroll
@@ -424,8 +591,18 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     __builtin_amdgcn_s_barrier();
     rdB(b1, cb, 1);
     if constexpr (Q4A) {
+      // tile t+1's A from its raw blocks (loaded in P2 of tile t-1), dequantized in P2 (the
+      // phase with the fewest LDS reads) into buffer cb^1: writable from P1 on (its last reads
+      // were P3 of tile t-1), the writes complete by the lgkmcnt(0) ending P3, before either
+      // wave group's first read of it in P1 of tile t+1.  Counted wait: the oldest loads in
+      // flight are tile t+1's raw blocks (2 per wave), then tile t+1's B pieces (4, P4 of tile
+      // t-1), which stay in flight.  The wait names the registers, so no use of them moves above it.
+      if (qown) asm volatile("s_waitcnt vmcnt(4)" : "+v"(qraw_n), "+v"(qd_n)::"memory");
+      qraw = qraw_n;
+      qd = qd_n;
+      qload(t + 2, qraw_n, qd_n);  // waited in P2 of tile t+1
 #pragma unroll
-      for (int w = 0; w < 4; ++w) qstore_word(cb ^ 1, w);  // (P2 reads the least: 4 B fragments)
+      for (int w = 0; w < 4; ++w) qstore_word(cb ^ 1, w);
       G2_SYNC_MMA(0, 1, b1)
     } else {
 #pragma unroll
@@ -437,10 +614,15 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
     if constexpr (Q4A) {
       G2_SYNC_MMA(1, 1, b1)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's A writes of tile t+1 landed
+      // tile t+1's B pieces landed; tile t+2's raw blocks (the 2 newest) stay in flight
+      if (qown)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       G2_SYNC_MMA(1, 1, b1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B pieces) landed
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (and tile t+1's B pieces) landed
     __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int p = AP; p < NPC; ++p) stage(t + 2, p);
@@ -451,170 +633,185 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
   if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMAs past the end have landed
   // C/D map of the 16x16 MFMA: column (token) = lane & 15, rows (weight rows) 4 * (lane >> 4) + reg
-  const int mw = m0 + wr * (BM / 2);  // the wave's first row
-  constexpr int MW = BM / 2;  // the wave's region: MW rows x 64 columns
-  if constexpr (GQ) {
-    // quantized fp16 values go through LDS too (as the f32 tile below): direct stores would
-    // write 32-byte pieces of 16 columns per instruction
-    constexpr int LDH = MW + 8;  // LDS row stride (halves, padded)
-    __syncthreads();
-    _Float16 *eh = g2lds + wave * 32 * LDH;
+  __syncthreads();  // (every wave is past its last LDS operand read)
+  g2_epilogue<GQ, EM, BM / 2, g2_lds_bytes(AP)>(acc, m0 + wr * (BM / 2), n0 + wc * 64, M, N, bias, Y, gelu_tab, Q16, epi,
+                                              g2lds, wave, lane);
+}
+
+// ================================================================== register-dequant prompt GEMM
+// k_gemm_q4r: the long-prompt GEMM with the weight operand dequantized straight into MFMA
+// registers, no LDS for A.  One 512-thread workgroup per 256 x 256 output tile; wave w owns
+// rows [32 w, 32 w + 32) -- one W4T32 tile, whose rows no other wave reads, so each weight
+// value is dequantized once per workgroup, as in the in-LDS variant, but without its LDS
+// stores (13 cycles per ds_write_b128) and the A fragment reads -- and all 256 columns.
+// A fragment (16 rows x 32 K of v_mfma_f32_16x16x32_f16): lane (fr, fk) holds 8 values of row
+// 16 i + fr at K offset 8 fk of block kk = word fk of that row's Q4_0 block, so a fragment is
+// one dword of nibbles and one scale per lane (16 rows x 16 bytes contiguous per load).
+// B (the fp16 activations): 4 pieces of 64 columns per K-tile, LDS-DMA into two buffers
+// (64 KB), XOR-swizzled as in k_gemm_f16_256.  Phase p of K-tile t (4 per K-tile): read
+// B piece p (8 fragments), dequantize fragment p of tile t+1, issue one B piece (piece p+2 of
+// tile t+1 for p < 2, piece p-2 of tile t+2 otherwise: restaged 2 phases after its last read)
+// and the raw loads of fragment p of tile t+3; barrier; 16 MFMAs (rows 2 x 16, columns of
+// piece p 4 x 16, K 2 x 32); wait; barrier.  Per wave and phase: 1 DMA then 2 raw loads, so
+// vmcnt(14) at the end of phase f retires the DMA of phase f-4 (read in phase f+2: one phase
+// after the wait, and one barrier more for the two staggered wave groups) and every raw load
+// up to phase f-5 (fragment loads are used 8 phases after their issue).  Raw loads ride in
+// two register sets by tile parity (the loop takes K-tiles in pairs: K % 128 == 0).
+constexpr int R_BM = 256;
+constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
+
+template <bool GQ, int EM>
+__global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, int K, const _Float16 *__restrict__ B,
+                                                             int N, const float *__restrict__ bias, float *__restrict__ Y,
+                                                             const uint16_t *__restrict__ gelu_tab,
+                                                             _Float16 *__restrict__ Q16, const G2Epi epi) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2;
+  const int tm = (M + R_BM - 1) / R_BM, tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (wg / tn) * R_BM, n0 = (wg % tn) * G2_BN;
+  const int nk = K / G2_BK, nb = K / QK;
+  const uint32_t lbase = lds_addr(g2lds);
+  auto stage = [&](int kt, int q) {  // B piece q of K-tile kt into buffer kt & 1 (clamped source tile)
+    const int kc = min(kt, nk - 1);
+    const int r = wave * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const int grow = min(n0 + q * 64 + r, N - 1);
+    glds16<false>(B + (size_t)grow * K + (size_t)kc * G2_BK + 8 * c,
+                  lbase + (uint32_t)((((kt & 1) * 4 + q) * G2_PIECE + wave * 8 * G2_BK) * 2));
+  };
+  const int fr = lane & 15, fk = lane >> 4;
+  const int qt = min(m0 / T32 + wave, (M + T32 - 1) / T32 - 1);  // (clamped: rows past M are not stored)
+  const uint8_t *qbase = WQ.qs + ((size_t)qt * nb * T32 + fr) * 16 + 4 * fk;
+  const float *dbase = WQ.d + (size_t)qt * nb * T32 + fr;
+  // raw fragment f = 2 i + kk of K-tile kt: word fk of block 2 kt + kk of row 16 i + fr, its scale
+  auto rload = [&](int kt, int f, uint32_t &w, float &d) {
+    const size_t o = (size_t)(2 * min(kt, nk - 1) + (f & 1)) * T32 + 16 * (f >> 1);
+    asm volatile("global_load_dword %0, %1, off" : "=v"(w) : "v"(qbase + o * 16) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(dbase + o) : "memory");
+  };
+  f32x4 acc[2][16];
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int p = 0; p < AP; ++p) {
-      const int mb = mw + 32 * p;  // the block's first row
-      float bv[8];
+    for (int j = 0; j < 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  uint32_t rw[2][4];
+  float rd[2][4];
+  half8 a[2][4], bq[4][2];
+  auto rdB = [&](int buf, int q) {
+    const _Float16 *bp = g2lds + (buf * 4 + q) * G2_PIECE;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bv[e] = mb + 4 * fk + e < M ? bias[mb + 4 * fk + e] : 0.0f;
-        bv[4 + e] = mb + 16 + 4 * fk + e < M ? bias[mb + 16 + 4 * fk + e] : 0.0f;
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 16 * jj + fr, c = kk * 4 + fk;
+        bq[jj][kk] = *(const half8 *)(bp + row * G2_BK + 8 * (c ^ (row & 7)));
       }
+  };
+  // prologue: raw tile 0 and fragments 0-1 of tile 1, then the ops of phases -6 and -5 of the
+  // loop's order; tile 0 dequantized; then phases -4 .. -1 (their raw loads reuse tile 0's set)
 #pragma unroll
-      for (int j = 2 * pass; j < 2 * pass + 2; ++j) {
-        float v[8];
+  for (int f = 0; f < 4; ++f) rload(0, f, rw[0][f], rd[0][f]);
+  rload(1, 0, rw[1][0], rd[1][0]);
+  rload(1, 1, rw[1][1], rd[1][1]);
+  stage(0, 0);
+  rload(1, 2, rw[1][2], rd[1][2]);
+  stage(0, 1);
+  rload(1, 3, rw[1][3], rd[1][3]);
+  asm volatile("s_waitcnt vmcnt(10)" : "+v"(rw[0][0]), "+v"(rw[0][1]), "+v"(rw[0][2]), "+v"(rw[0][3]), "+v"(rd[0][0]),
+               "+v"(rd[0][1]), "+v"(rd[0][2]), "+v"(rd[0][3])::"memory");
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = h2f(gelu_tab[f2h(acc[2 * p][j][e] + bv[e])]);
-          v[4 + e] = h2f(gelu_tab[f2h(acc[2 * p + 1][j][e] + bv[4 + e])]);
-        }
-        float amax = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) amax = amax > fabsf(v[e]) ? amax : fabsf(v[e]);
-        float o = __shfl_xor(amax, 16, 64);
-        amax = amax > o ? amax : o;
-        o = __shfl_xor(amax, 32, 64);
-        amax = amax > o ? amax : o;
-        const float d = amax / 7.0f;
-        const float id = d != 0.0f ? 1.0f / d : 0.0f;
-        _Float16 h[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) h[e] = (_Float16)(d * (float)(x86_round_i8(v[e] * id)));
-        _Float16 *row = eh + ((j & 1) * 16 + fr) * LDH + 32 * p + 4 * fk;
-        *(uint2 *)row = *(const uint2 *)&h[0];
-        *(uint2 *)(row + 16) = *(const uint2 *)&h[4];
-      }
-    }
-    // (M % 32 == 0: a chunk of 8 rows is wholly in or out)
-    for (int idx = lane; idx < 32 * (MW / 8); idx += 64) {
-      const int nl = idx / (MW / 8), c = idx % (MW / 8);
-      const int n = n0 + wc * 64 + 32 * pass + nl, m = mw + 8 * c;
-      const uint4 v = *(const uint4 *)(eh + nl * LDH + 8 * c);
-      if (n < N && m < M) *(uint4 *)(Q16 + (size_t)n * M + m) = v;
-    }
-    }
-    return;
+  for (int f = 0; f < 4; ++f) a[0][f] = deq_word_f16(rw[0][f], rd[0][f]);
+  stage(0, 2);
+  rload(2, 0, rw[0][0], rd[0][0]);
+  stage(0, 3);
+  rload(2, 1, rw[0][1], rd[0][1]);
+  stage(1, 0);
+  rload(2, 2, rw[0][2], rd[0][2]);
+  stage(1, 1);
+  rload(2, 3, rw[0][3], rd[0][3]);
+  asm volatile("s_waitcnt vmcnt(14)" : "+v"(rw[1][0])::"memory");  // B pieces 0, 1 of tile 0
+  __builtin_amdgcn_s_barrier();
+  if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+  // one phase: P = t & 1 (the parity of K-tile t), p = 0..3
+#define R_PHASE(t, P, p)                                                                                       \
+  {                                                                                                            \
+    rdB(P, p);                                                                                                 \
+    a[(P) ^ 1][p] = deq_word_f16(rw[(P) ^ 1][p], rd[(P) ^ 1][p]);                                              \
+    stage((p) < 2 ? (t) + 1 : (t) + 2, ((p) + 2) & 3);                                                         \
+    rload((t) + 3, p, rw[(P) ^ 1][p], rd[(P) ^ 1][p]);                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                                         \
+    __builtin_amdgcn_s_barrier();                                                                              \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                         \
+    __builtin_amdgcn_s_setprio(1);                                                                             \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                           \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                            \
+        _Pragma("unroll") for (int jj = 0; jj < 4; ++jj)                                                       \
+          acc[i][4 * (p) + jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[P][2 * i + kk], bq[jj][kk],          \
+                                                                        acc[i][4 * (p) + jj], 0, 0, 0);        \
+    __builtin_amdgcn_s_setprio(0);                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                         \
+    if ((p) < 3)                                                                                               \
+      asm volatile("s_waitcnt vmcnt(14)" : "+v"(rw[(P) ^ 1][((p) + 1) & 3]), "+v"(rd[(P) ^ 1][((p) + 1) & 3])::"memory"); \
+    else                                                                                                       \
+      asm volatile("s_waitcnt vmcnt(14)" : "+v"(rw[P][0]), "+v"(rd[P][0])::"memory");                          \
+    __builtin_amdgcn_s_barrier();                                                                              \
   }
-  // The f32 tile leaves through LDS: a lane's accumulator holds 4 consecutive rows m of one
-  // column n, so direct stores write 16 columns x 64 bytes per instruction; each wave instead
-  // writes its (BM/2) x 64 region into its own LDS area, CP columns at a time, and stores
-  // whole runs of (BM/2) floats per column (the direct stores cost 8-10 % of the GEMM).
-  constexpr int LDW = MW + 4;  // LDS row stride (floats, padded)
-  constexpr int CP = 8 * 32 * LDW * 4 <= 2 * NPC * G2_PIECE * 2 ? 32 : 16;  // columns per pass
-  __syncthreads();                           // (every wave is past its last LDS operand read)
-  float *ep = (float *)g2lds + wave * CP * LDW;
-  const bool vec = (M & 3) == 0;
-#pragma unroll
-  for (int pass = 0; pass < 64 / CP; ++pass) {
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int jj = 0; jj < CP / 16; ++jj)
-        *(f32x4 *)(ep + (16 * jj + fr) * LDW + 16 * i + 4 * fk) = acc[i][(CP / 16) * pass + jj];
-    // (a wave's own LDS writes and reads are ordered)
-    constexpr int RW = MW / 4, NIT = CP * RW / 64;  // float4 chunks per column run; per lane
-    static_assert(CP * RW % 64 == 0, "whole chunks per lane");
-    // the epilogue's extra inputs, all loaded before the pass's first store (Y may be epi.res,
-    // and a load behind a store it may alias waits for it: one exposed latency per chunk)
-    [[maybe_unused]] f32x4 xr[EM == 2 ? NIT : 1], xa[EM == 2 ? NIT : 1];
-    [[maybe_unused]] double2 cq[EM == 1 ? NIT : 1][2];
-    if constexpr (EM != 0) {
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
-        const int n = n0 + wc * 64 + CP * pass + nl, m = mw + 4 * c;
-        if (n >= N || m >= M) continue;
-        if constexpr (EM == 2) {
-          xr[it] = *(const f32x4 *)(epi.res + (size_t)n * M + m);
-          if (epi.res_a) xa[it] = *(const f32x4 *)(epi.res_a + (size_t)n * M + m);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int dd = (m + 2 * q) % epi.d;
-            cq[it][q] = dd < epi.n_rot ? epi.cs[(size_t)(epi.p0 + n) * (epi.n_rot / 2) + dd / 2] : make_double2(1.0, 0.0);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
-      const int n = n0 + wc * 64 + CP * pass + nl, m = mw + 4 * c;
-      f32x4 v = *(const f32x4 *)(ep + nl * LDW + 4 * c);
-      if (n >= N || m >= M) continue;
-      if (bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += m + e < M ? bias[m + e] : 0.0f;
-      }
-      if constexpr (EM == 1) {  // (the launcher guarantees M % 4 == 0 and an even d: pairs stay in the run)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          if ((m + 2 * q) % epi.d < epi.n_rot) {
-            const double2 cs = cq[it][q];
-            const double x0 = v[2 * q], x1 = v[2 * q + 1];
-            v[2 * q] = (float)(x0 * cs.x - x1 * cs.y);
-            v[2 * q + 1] = (float)(x0 * cs.y + x1 * cs.x);
-          }
-        }
-        if (epi.h16) {
-          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-          *(h4 *)(epi.h16 + (size_t)(epi.p0 + n) * M + m) = (h4){(_Float16)v[0], (_Float16)v[1], (_Float16)v[2],
-                                                                 (_Float16)v[3]};
-        }
-      }
-      if constexpr (EM == 2) {
-        if (epi.res_a) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = xr[it][e] + (xa[it][e] + v[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] + xr[it][e];
-        }
-      }
-      float *dst = Y + (size_t)n * M + m;
-      if (vec && m + 3 < M) {
-        *(f32x4 *)dst = v;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (m + e < M) dst[e] = v[e];
-      }
-    }
-    if constexpr (EM == 3) {
-      // the pass's columns again, read down the LDS region: runs of 8 columns of one row m,
-      // as fp16, into row m of the transposed copy (4 lanes cover a row's 32 columns)
-      constexpr int C8 = CP / 8, NT2 = MW * C8 / 64;
-      static_assert(MW * C8 % 64 == 0, "whole runs per lane");
-#pragma unroll
-      for (int it = 0; it < NT2; ++it) {
-        const int idx = lane + 64 * it, c8 = idx % C8, ml = idx / C8;
-        const int m = mw + ml, nb = n0 + wc * 64 + CP * pass + 8 * c8;
-        if (m >= M || nb >= N) continue;
-        const float bm = bias ? bias[m] : 0.0f;
-        half8 h;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) h[j] = (_Float16)(ep[(8 * c8 + j) * LDW + ml] + bm);
-        _Float16 *dst = epi.h16 + (size_t)m * epi.h16_ld + epi.p0 + nb;
-        if (nb + 8 <= N && ((epi.p0 + nb) & 7) == 0) {
-          *(half8 *)dst = h;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (nb + j < N) dst[j] = h[j];
-        }
-      }
-    }
+  for (int t = 0; t < nk; t += 2) {
+    R_PHASE(t, 0, 0)
+    R_PHASE(t, 0, 1)
+    R_PHASE(t, 0, 2)
+    R_PHASE(t, 0, 3)
+    R_PHASE(t + 1, 1, 0)
+    R_PHASE(t + 1, 1, 1)
+    R_PHASE(t + 1, 1, 2)
+    R_PHASE(t + 1, 1, 3)
   }
+#undef R_PHASE
+  if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped loads past the end have landed
+  __syncthreads();
+  // the wave's 32 rows x 256 columns as four 32 x 64 regions
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 aq[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) aq[i][j] = acc[i][4 * q + j];
+    g2_epilogue<GQ, EM, 32, r_lds_bytes()>(aq, m0 + 32 * wave, n0 + 64 * q, M, N, bias, Y, gelu_tab, Q16, epi, g2lds,
+                                           wave, lane);
+  }
+}
+
+template <bool GQ, int EM>
+static void r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, const uint16_t *tab,
+                 void *q16, const G2Epi &epi, hipStream_t s) {
+  const int nwg = ((M + R_BM - 1) / R_BM) * ((n + G2_BN - 1) / G2_BN);
+  hipLaunchKernelGGL((k_gemm_q4r<GQ, EM>), dim3(nwg), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K, (const _Float16 *)x16,
+                     n, bias, y, tab, (_Float16 *)q16, epi);
+}
+
+static int r_launch(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, hipStream_t s,
+                    const uint16_t *tab, void *q16, const G2Epi &epi) {
+  static bool attr = false;
+  if (!attr) {
+    const void *fns[] = {(const void *)k_gemm_q4r<false, 0>, (const void *)k_gemm_q4r<false, 1>,
+                         (const void *)k_gemm_q4r<false, 2>, (const void *)k_gemm_q4r<false, 3>,
+                         (const void *)k_gemm_q4r<true, 0>};
+    for (const void *f : fns)
+      VSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
+    attr = true;
+  }
+  if (q16) r_go<true, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else if (epi.cs) r_go<false, 1>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else if (epi.res) r_go<false, 2>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else if (epi.h16) r_go<false, 3>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else r_go<false, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
 }
 
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s) {
@@ -677,6 +874,16 @@ int launch_gemm_q4_256(const W4 &W, const void *x16, int n, const float *bias, f
   return g2_checked(nullptr, &W, W.rows, W.k, x16, n, bias, y, s, q16, epi);
 }
 
+// the register-dequant kernel for every Q4_0 weight with K % 128 == 0 (VSIM_Q4R=0: A/B builds
+// that keep the in-LDS dequant kernel).  Measured at the codegen-16B shapes (N = 2048,
+// tools/gemm_bench.py): 24576 x 6144 941 -> 964-972 TFLOP/s, 6144 x 24576 893-898 -> 916,
+// 6144 x 6144 803 -> 811-824 even though its 192 tiles of 256 rows leave 64 CUs idle (the
+// in-LDS kernel's 256 tiles of 192 rows fill them).
+#ifndef VSIM_Q4R
+#define VSIM_Q4R 1
+#endif
+static bool r_use(int K) { return VSIM_Q4R && K % (2 * G2_BK) == 0; }
+
 static int g2_checked(const void *A16, const W4 *WQ, int M, int K, const void *x16, int n, const float *bias, float *y,
                       hipStream_t s, void *q16, const G2Epi *epi) {
   if (K % G2_BK || K <= 0 || M <= 0 || n <= 0 || (q16 && (M % QK || !bias))) {
@@ -698,6 +905,7 @@ static int g2_checked(const void *A16, const W4 *WQ, int M, int K, const void *x
     if (int rc = tables_get(&t)) return rc;
     tab = t.gelu_f16;
   }
+  if (WQ && r_use(K)) return r_launch(*WQ, M, K, x16, n, bias, y, s, tab, q16, e);
   if (WQ) {
     return g2_ap(M, n) == 3 ? g2_launch<3, true>(nullptr, *WQ, M, K, x16, n, bias, y, s, tab, q16, e)
                             : g2_launch<4, true>(nullptr, *WQ, M, K, x16, n, bias, y, s, tab, q16, e);

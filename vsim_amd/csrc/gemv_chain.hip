@@ -292,27 +292,39 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
 // each, so the activation factors are wave-uniform scalar loads and the LDS carries
 // nothing but pair terms.  Waves the hardware would place on SIMD0 (4, 8, ...) only join
 // the barriers.  Weights: register ring as k_gemv_chain2.
-template <int CB>
+// CONS = 2: 128 rows per workgroup, two consumer waves (0 and 4: the waves of a workgroup go
+// to the SIMDs cyclically, so these two share one SIMD, where two independent chains
+// interleave without stretching each other) and 2 CB producers on the other three SIMDs
+// (wave 8 and 12 join the barriers only), the LDS ring for 128 rows (153.6 KB at CB = 6:
+// one workgroup per CU by construction, so no other workgroup's producers land on the
+// consumers' SIMD).
+template <int CB, int CONS = 1>
 struct SoloShape {
   static constexpr int CP = CB * 16, LD = CP + 4;
-  static constexpr int WAVES = 1 + CB + (CB - 1) / 3;  // consumer, producers, SIMD0 fillers
+  static constexpr int PRODUCERS = CB * CONS;
+  // waves with index = 0 mod 4 share the consumers' SIMD: the first CONS are the consumers,
+  // the rest only join the barriers; the others are the producers
+  static constexpr int WAVES = PRODUCERS + (PRODUCERS + 2) / 3;  // a 0-mod-4 slot per 3 producers
+  static constexpr int ROWS = 64 * CONS;
   static constexpr int WIN = CP / 4 % 8 == 0 ? 8 : 12;
   static_assert(CP / 4 % WIN == 0, "the read window must tile the chunk");
   static_assert(WAVES <= 16, "workgroup size");
+  static_assert((WAVES + 3) / 4 >= CONS, "consumer waves on one SIMD");
 };
 constexpr int C5_RING = 3;
 
 // PF: prefetch distance of the weight loads in chunks (register ring of PF+1 sets)
-// One 64-row group g of batch B (groups numbered job by job); P: the pair-term ring.
+// One ROWS-row group g of batch B (groups numbered job by job); P: the pair-term ring.
 // Every wave returns from here (producers and fillers early); all take nit barriers.
-template <int CB, int PF>
-__device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[64 * SoloShape<CB>::LD]) {
-  using S = SoloShape<CB>;
+template <int CB, int PF, int CONS>
+__device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD]) {
+  using S = SoloShape<CB, CONS>;
+  constexpr int TPG = 2 * CONS;  // 32-row tiles per group
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   int ji = 0;
   while (ji < B.nj) {
-    const int ng = (B.j[ji].w.tiles + 1) / 2;
+    const int ng = (B.j[ji].w.tiles + TPG - 1) / TPG;
     if (g < ng) break;
     g -= ng;
     ++ji;
@@ -323,15 +335,16 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
   const int nit = (nch + 2 + PF) / (PF + 1) * (PF + 1);
 
-  if (wave != 0 && (wave & 3) == 0) {  // SIMD0 filler
+  if ((wave & 3) == 0 && (wave >> 2) >= CONS) {  // filler on the consumers' SIMD
     for (int k = 0; k < nit; ++k) __syncthreads();
     return;
   }
-  if (wave > 0) {
+  if ((wave & 3) != 0) {
     // ------------------------------------------------------------- producer
-    const int o = wave - 1 - (wave >> 2);  // 1,2,3,5,6,7,9,... -> 0,1,2,...
+    const int pi = wave - 1 - (wave >> 2);  // 1,2,3,5,6,7,9,... -> 0,1,2,...
+    const int o = pi % CB, c = pi / CB;     // block of the chunk, consumer (64-row half) served
     const int h = lane >> 5, r = lane & 31;
-    const int tile = 2 * g + h;
+    const int tile = TPG * g + 2 * c + h;
     const bool tile_ok = tile < tiles;
     const int tl = tile_ok ? tile : tiles - 1;
     const uint8_t *qs = B.j[ji].w.qs + ((size_t)tl * nb * T32 + r) * 16;
@@ -361,6 +374,7 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
       __builtin_amdgcn_sched_barrier(0);
       ldx(k + 1, xn);
       __builtin_amdgcn_sched_barrier(0);
+#ifndef VSIM_SOLO_NOPROD  // (A/B experiment builds: loads and barriers only)
       {
         const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
         const float dl = 512.0f * dv, ml = -8.0f * dv;
@@ -368,7 +382,7 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
         asm("v_mov_b32 %0, %1" : "=v"(dh) : "v"(dl));  // see k_gemv_chain2
         asm("v_mov_b32 %0, %1" : "=v"(mh) : "v"(ml));
         const f32x2 d2 = {dl, dh}, m2 = {ml, mh};
-        float *dst = &P[ps][lane * S::LD + o * 16];
+        float *dst = &P[ps][(64 * c + lane) * S::LD + o * 16];
 #pragma unroll
         for (int wv = 0; wv < 4; ++wv) {
           float p4[4];
@@ -376,6 +390,7 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
           *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
         }
       }
+#endif
       ps = ps == C5_RING - 1 ? 0 : ps + 1;
       __builtin_amdgcn_sched_barrier(0);
       producer_barrier();
@@ -402,7 +417,8 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   // --------------------------------------------------------------- consumer
   float acc = 0.0f;
   float4 win[S::WIN];
-  auto src = [&](int c) { return &P[c % C5_RING][lane * S::LD]; };
+  const int crow = 64 * wave / 4 + lane;  // this consumer's row within the group
+  auto src = [&](int c) { return &P[c % C5_RING][crow * S::LD]; };
   __builtin_amdgcn_s_setprio(3);
   for (int k = 0; k < nit; ++k) {
     const int c = k - 2;
@@ -415,10 +431,14 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
 #pragma unroll
       for (int j = 0; j < S::CP / 4; ++j) {
         const float4 v = win[j % S::WIN];
+#ifdef VSIM_SOLO_NOCHAIN  // (A/B experiment builds: the reads without the dependent adds)
+        acc = fmaxf(acc, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+#else
         acc = acc + v.x;
         acc = acc + v.y;
         acc = acc + v.z;
         acc = acc + v.w;
+#endif
         const int jn = j + S::WIN;
         win[j % S::WIN] = jn < S::CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - S::CP / 4));
         __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
@@ -429,7 +449,7 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   }
 
   // ----------------------------------------------------------------- epilogue
-  const int row = g * 64 + lane;
+  const int row = g * S::ROWS + crow;
   const int rows = B.j[ji].w.rows;
   const float *bias = B.j[ji].bias;
   float *y = B.j[ji].y;
@@ -449,15 +469,15 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int CB, int PF>
-__global__ void __launch_bounds__(64 * SoloShape<CB>::WAVES, 1) k_gemv_solo(GemvBatch B) {
-  __shared__ __attribute__((aligned(16))) float P[C5_RING][64 * SoloShape<CB>::LD];
-  solo_body<CB, PF>(B, blockIdx.x, P);
+template <int CB, int PF, int CONS>
+__global__ void __launch_bounds__((64 * SoloShape<CB, CONS>::WAVES), 1) k_gemv_solo(GemvBatch B) {
+  __shared__ __attribute__((aligned(16))) float P[C5_RING][SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD];
+  solo_body<CB, PF, CONS>(B, blockIdx.x, P);
 }
 
-static int solo_groups(const GemvBatch &B) {
+static int solo_groups(const GemvBatch &B, int cons = 1) {
   int g = 0;
-  for (int i = 0; i < B.nj; ++i) g += (B.j[i].w.tiles + 1) / 2;
+  for (int i = 0; i < B.nj; ++i) g += (B.j[i].w.tiles + 2 * cons - 1) / (2 * cons);
   return g;
 }
 
@@ -466,8 +486,14 @@ static int solo_groups(const GemvBatch &B) {
 // them to cover the CUs, else 32-row workgroups (k_gemv_chain32: more CUs per row, for
 // fc_out and the out-projection, whose K = 4E chains are the whole cost).
 constexpr int SOLO_CB = 6, SOLO_PF = 3, SOLO_MIN_GROUPS = 192;
+#ifndef VSIM_SOLO_CONS2  // (A/B experiment builds: 0 keeps every batch on the 64-row groups)
+#define VSIM_SOLO_CONS2 0
+#endif
 
 bool gemv_chain_solo(const GemvBatch &B) { return solo_groups(B) >= SOLO_MIN_GROUPS; }
+// 128-row groups when they still cover most CUs (the Q, K, V + fc_in batch: 224 groups in one
+// round instead of 448 at two per CU)
+static bool solo_cons2(const GemvBatch &B) { return VSIM_SOLO_CONS2 && solo_groups(B, 2) >= SOLO_MIN_GROUPS; }
 
 int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
   int tiles = 0;
@@ -480,9 +506,15 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     tiles += B.j[i].w.tiles;
   }
   if (tiles == 0) return VSIM_OK;
-  const int groups = solo_groups(B);
-  if (gemv_chain_solo(B)) {
-    hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF>), dim3(groups), dim3(64 * SoloShape<SOLO_CB>::WAVES), 0, s, B);
+  if (solo_cons2(B)) {
+    hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 2>), dim3(solo_groups(B, 2)),
+                       dim3(64 * SoloShape<SOLO_CB, 2>::WAVES), 0, s, B);
+  } else if (gemv_chain_solo(B)) {
+#ifndef VSIM_SOLO_LDS_PAD  // (A/B experiment builds: dynamic LDS that limits workgroups per CU)
+#define VSIM_SOLO_LDS_PAD 0
+#endif
+    hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)), dim3(64 * SoloShape<SOLO_CB, 1>::WAVES),
+                       VSIM_SOLO_LDS_PAD, s, B);
   } else {
     hipLaunchKernelGGL(k_gemv_chain32, dim3(tiles), dim3(C2_THREADS), 0, s, B);
   }
