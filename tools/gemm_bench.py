@@ -42,7 +42,7 @@ for M, K in shapes:
     fq = lambda: hip.check(L.vsim_op_gemm_q4_256(w.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None, None,
                                                  0, 0, 0, 0, None, None), "q4")
     fi = lambda: hip.check(L.vsim_op_gemm_f16(img.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None), "img")
-    for name, f in (("q4 in-LDS dequant", fq), ("fp16 image", fi)):
+    for name, f in (("q4 (model kernel)", fq), ("fp16 image", fi)):
         ms = timeit(f)
         print(f"M={M} K={K} N={N} {name:18s}: {ms * 1e3:.1f} us  {2.0 * M * K * N / ms / 1e9:.0f} TFLOP/s", flush=True)
     del aos, w, img, x, y
