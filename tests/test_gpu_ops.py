@@ -148,6 +148,57 @@ def test_norm_fallback_paths():
     assert np.array_equal(bits(host(y)), bits(ref))
 
 
+@pytest.mark.parametrize("n", [4096, 4160, 1024])
+def test_norm_sequential_mean_sum_cases(n):
+    """The LayerNorm's fallback for rows whose mean sum is not provably order-independent
+    (kern.hpp seq_sum_exact: per-256 chunk certificates, exact prefix sums, speculation from
+    the running sum checked by TwoSum, lane-0 order where a chunk fails): rows with one or a
+    few tiny elements (the common case: no restart), many tiny elements in one chunk (more
+    roundings than the restart cap), a huge dynamic range inside a chunk (its certificate
+    fails), denormals, zeros, a large running sum that rounds as it grows, exact cancellations,
+    a partial last chunk (n = 4160).  Every row against the oracle's sequential sum, bit for bit."""
+    import oracle_py as O
+    rng = np.random.default_rng(n)
+    rows = []
+    for k in range(48):
+        r = (rng.standard_normal(n) * rng.choice([0.05, 1.0, 40.0])).astype(np.float32)
+        kind = k % 8
+        if kind == 0:
+            r[rng.integers(0, n)] = np.float32(3e-7) * np.float32(rng.standard_normal())
+        elif kind == 1:
+            r[rng.integers(0, n, 5)] = (rng.standard_normal(5) * 1e-9).astype(np.float32)
+        elif kind == 2:
+            c = rng.integers(0, n // 256) * 256
+            r[c:c + 200] = (rng.standard_normal(200) * 1e-12).astype(np.float32)  # > the cap in one chunk
+        elif kind == 3:
+            r[rng.integers(0, n, 3)] = np.float32(1e30)
+            r[rng.integers(0, n, 3)] = np.float32(1e-30)
+        elif kind == 4:
+            r[rng.integers(0, n, 7)] = np.float32(1e-41)  # denormals
+            r[rng.integers(0, n, 50)] = np.float32(0.0)
+        elif kind == 5:
+            r = (np.abs(r) * 1000 + 1e-4 * rng.standard_normal(n)).astype(np.float32)  # growing running sum
+        elif kind == 6:
+            r[1::2] = -r[0::2]  # exact cancellation pairs ...
+            r[rng.integers(0, n)] = np.float32(1e-8)  # ... and one tiny element
+        else:
+            r[rng.integers(0, n, 40)] *= np.float32(1e-7)
+        rows.append(r)
+    x = np.concatenate(rows).astype(np.float32)
+    ref = O.norm(x, n, len(rows))
+    xt = dev(x)
+    y = torch.empty_like(xt)
+    g = torch.zeros(64, device=DEV)  # (an op that fetches the device tables also sets up the fallback counters)
+    hip.check(hip.lib().vsim_op_gelu(g.data_ptr(), g.data_ptr(), g.numel(), None), "gelu")
+    torch.cuda.synchronize()
+    before = hip.norm_fallbacks()[0]
+    hip.check(hip.lib().vsim_op_norm(xt.data_ptr(), y.data_ptr(), n, len(rows), None, None, None), "norm")
+    got = host(y).reshape(len(rows), n)
+    bad = [i for i in range(len(rows)) if not np.array_equal(bits(got[i]), bits(ref.reshape(len(rows), n)[i]))]
+    assert not bad, f"rows {bad} differ"
+    assert hip.norm_fallbacks()[0] > before  # the fallback path ran
+
+
 def test_gelu_bit_exact():
     z = ops("gelu")
     x = dev(z["x"])
@@ -460,11 +511,12 @@ def test_prefill_gemm_q4_in_lds_dequant_bit_identical(M, K, N):
                                              None), init=R)
 
 
-@pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])
+@pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (256, 3, 300, 37), (256, 1, 64, 130), (256, 2, 1100, 40),
+                                           (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])
 def test_attn_prefill_f16(d, H, N, n_past):
-    """Fast-mode prompt attention (attn_prefill.hip) against fp64 causal attention:
-    scores and probabilities pass through fp16, so the tolerance is 2e-2 of max|V| (the
-    observed error is ~1e-3)."""
+    """Fast-mode prompt attention (attn_prefill.hip; d = 256 on the two-waves-per-group kernel)
+    against fp64 causal attention: scores and probabilities pass through fp16, so the tolerance
+    is 2e-2 of max|V| (the observed error is ~1e-3).  Ragged N, a cache before the prompt."""
     rng = np.random.default_rng(d + N + n_past)
     E, nk = d * H, n_past + N
     Q = rng.standard_normal((N, E)).astype(np.float32)
