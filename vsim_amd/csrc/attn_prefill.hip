@@ -296,6 +296,178 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
   }
 }
 
+// D = 256, two waves per query group: k_attn_prefill_f16 at D = 256 holds a 32-query group's
+// Q fragments (64 VGPRs), its 256 x 32 O^T accumulators (128) and both S^T tiles in one wave,
+// 472 registers: one wave per SIMD, every latency exposed.  Here a workgroup is 8 waves for
+// the same 128 queries; waves g and g + 4 share query group g and split each 64-key block:
+//  * S^T: wave half c computes keys 32 c .. 32 c + 31 (one 32 x 32 tile, 16 MFMAs over D);
+//  * the block maximum of each query goes through LDS to the partner, so both take the same
+//    new running maximum and rescale factor (the same operations on the same values);
+//  * each wave turns its tile into P^T (the next MFMA's B operand, as above) and stores it
+//    for the partner (lane-linear: the partner's lane l needs exactly lane l's values);
+//  * O^T: wave half c accumulates dims 128 c .. 128 c + 127 over all 64 keys (4 tiles x 4
+//    K-steps: its own P^T for its keys, the partner's for the others).
+// Each wave keeps the running sum of its own keys' probabilities; the two partial sums are
+// added (half 0's first) at the end.  ≈190 registers: two waves per SIMD.  Barriers per key
+// block: after the maxima, after the P^T stores, after the next tile's DMA (as above).
+constexpr int AP2_THREADS = 512;
+constexpr size_t ap2_lds() { return (size_t)2 * 2 * AP_BK * 256 * sizeof(_Float16) + 4 * 2 * 2 * 64 * 16 + 4 * 2 * 64 * 4; }
+
+__global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const float *__restrict__ Q,
+                                                                       const _Float16 *__restrict__ k16,
+                                                                       const _Float16 *__restrict__ vt16, int E, int H,
+                                                                       int N, int n_past, int ldt, float qscale,
+                                                                       float *__restrict__ out) {
+  constexpr int D = 256;
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  // [0, 128 KB): K and V^T tiles, two buffers each (as k_attn_prefill_f16's D = 256 path);
+  // then the P^T exchange [group][half][s2][lane] (16 B) and the maxima / sums [group][half][lane]
+  u32x4 *pex = (u32x4 *)(lds + 2 * 2 * AP_BK * D);
+  float *mex = (float *)(pex + 4 * 2 * 2 * 64);
+  const int nqb = (N + AP_BQ - 1) / AP_BQ;
+  const int h = blockIdx.x % H, q0 = (nqb - 1 - (int)blockIdx.x / H) * AP_BQ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wv & 3, half = wv >> 2;
+  const int r = lane & 31, hl = lane >> 5;
+  const int qw = q0 + grp * 32;
+  const int myq = qw + r;
+  const _Float16 *kbase = k16 + (size_t)h * D, *vbase = vt16 + (size_t)h * D * ldt;
+  ahalf8 qf[D / 16];
+  {
+    const float *qr = Q + (size_t)min(myq, N - 1) * E + h * D;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const float4 a = *(const float4 *)(qr + 16 * s + 8 * hl), b = *(const float4 *)(qr + 16 * s + 8 * hl + 4);
+      ahalf8 f;
+      f[0] = (_Float16)(a.x * qscale);
+      f[1] = (_Float16)(a.y * qscale);
+      f[2] = (_Float16)(a.z * qscale);
+      f[3] = (_Float16)(a.w * qscale);
+      f[4] = (_Float16)(b.x * qscale);
+      f[5] = (_Float16)(b.y * qscale);
+      f[6] = (_Float16)(b.z * qscale);
+      f[7] = (_Float16)(b.w * qscale);
+      qf[s] = f;
+    }
+  }
+  af32x16 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = (af32x16){};
+  float mrow = -INFINITY, lrow = 0.0f;
+  const int klast = n_past + min(q0 + AP_BQ, N) - 1;
+  const int nkb = klast / AP_BK + 1;
+  const uint32_t lb = lds_addr(lds);
+  auto gl_stage = [&](int kb, int buf) __attribute__((always_inline)) {
+    const int k0 = kb * AP_BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // K: 2 rows (keys) per wave instruction
+      const int row0 = (j * 8 + wv) * 2, row = row0 + (lane >> 5);
+      const int c = (lane & 31) ^ (row & 15);
+      glds16<false>(kbase + (size_t)min(k0 + row, klast) * E + 8 * c,
+                    lb + (uint32_t)((buf * AP_BK * D + row0 * D) * 2));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // V^T: 8 rows (dims) per wave instruction
+      const int row0 = (j * 8 + wv) * 8, row = row0 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      glds16<false>(vbase + (size_t)row * ldt + k0 + 8 * c,
+                    lb + (uint32_t)((2 * AP_BK * D + buf * D * AP_BK + row0 * AP_BK) * 2));
+    }
+  };
+  gl_stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * AP_BK, buf = kb & 1;
+    if (kb + 1 < nkb) gl_stage(kb + 1, buf ^ 1);
+    const _Float16 *Ks = lds + buf * AP_BK * D;
+    const _Float16 *Vt = lds + 2 * AP_BK * D + buf * D * AP_BK;
+    const bool vis = k0 <= n_past + min(qw + 31, N - 1);  // uniform over the pair
+    af32x16 st = (af32x16){};
+    if (vis) {
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        const int krow = 32 * half + r;
+        const ahalf8 kf = *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))];
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st, 0, 0, 0);
+        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      float bm = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int key = k0 + 32 * half + (g & 3) + 8 * (g >> 2) + 4 * hl;
+        if (key > n_past + myq) st[g] = -INFINITY;
+        bm = fmaxf(bm, st[g]);
+      }
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      mex[(grp * 2 + half) * 64 + lane] = bm;
+    }
+    __syncthreads();
+    if (vis) {
+      const float mnew = fmaxf(mrow, fmaxf(mex[(grp * 2) * 64 + lane], mex[(grp * 2 + 1) * 64 + lane]));
+      const float alpha = mnew == -INFINITY ? 1.0f : exp2f(mrow - mnew);
+      float ls = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float pv = st[g] == -INFINITY ? 0.0f : exp2f(st[g] - mnew);
+        st[g] = pv;
+        ls += pv;
+      }
+      ls += __shfl_xor(ls, 32, 64);
+      lrow = lrow * alpha + ls;
+      mrow = mnew;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = o[i] * alpha;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        ahalf8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (_Float16)st[8 * s2 + j];
+        pex[((grp * 2 + half) * 2 + s2) * 64 + lane] = *(const u32x4 *)&pf;
+      }
+    }
+    __syncthreads();
+    if (vis) {
+      // O^T dims 128 half + 32 i, keys 32 t + 16 s2 + ...: P^T of tile t from wave half t
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const u32x4 pw = pex[((grp * 2 + t) * 2 + s2) * 64 + lane];
+          const ahalf8 pf = *(const ahalf8 *)&pw;
+          const int kbase2 = 32 * t + 16 * s2 + 4 * hl;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int vrow = 128 * half + 32 * i + r, vc = kbase2 >> 3;
+            const _Float16 *vr = &Vt[vrow * AP_BK + 8 * (vc ^ ((vrow >> 1) & 7)) + 4 * hl];
+            const _Float16 *vr1 = &Vt[vrow * AP_BK + 8 * ((vc + 1) ^ ((vrow >> 1) & 7)) + 4 * hl];
+            const ahalf4 v0 = *(const ahalf4 *)vr, v1 = *(const ahalf4 *)vr1;
+            const ahalf8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
+          }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile has landed
+    __syncthreads();
+  }
+  // the running sums of both halves (half 0's + half 1's, in that order, in both waves)
+  mex[(grp * 2 + half) * 64 + lane] = lrow;
+  __syncthreads();
+  const float lt = mex[(grp * 2) * 64 + lane] + mex[(grp * 2 + 1) * 64 + lane];
+  if (myq < N) {
+    const float inv = 1.0f / lt;
+    float *orow = out + (size_t)myq * E + h * D + 128 * half;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * i + 8 * g + 4 * hl;
+        *(float4 *)(orow + dd) = make_float4(o[i][4 * g] * inv, o[i][4 * g + 1] * inv, o[i][4 * g + 2] * inv,
+                                             o[i][4 * g + 3] * inv);
+      }
+  }
+}
+
 bool attn_prefill_supported(int d) { return d == 64 || d == 96 || d == 128 || d == 256; }
 
 template <int D>
@@ -341,6 +513,22 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
     VSIM_HIP(hipFuncSetAttribute((const void *)k_attn_prefill_f16<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)attn_prefill_lds<256>()));
     attr = true;
+  }
+#ifndef VSIM_ATTN_PAIR  // (A/B builds: 0 keeps D = 256 on the one-wave-per-group kernel)
+#define VSIM_ATTN_PAIR 1
+#endif
+  if (VSIM_ATTN_PAIR && d == 256) {
+    static bool attr2 = false;
+    if (!attr2) {
+      VSIM_HIP(hipFuncSetAttribute((const void *)k_attn_prefill_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)ap2_lds()));
+      attr2 = true;
+    }
+    hipLaunchKernelGGL(k_attn_prefill_pair, grid, dim3(AP2_THREADS), ap2_lds(), s, Q, k16, vt16, E, H, N, n_past, ldt,
+                       qscale, out);
+    VSIM_HIP(hipGetLastError());
+    if (own) VSIM_HIP(hipFreeAsync(buf, s));
+    return VSIM_OK;
   }
 #define APL(DD)                                                                                                   \
   hipLaunchKernelGGL(k_attn_prefill_f16<DD>, grid, dim3(AP_THREADS), attn_prefill_lds<DD>(), s, Q, k16, vt16, E, H, \

@@ -161,6 +161,96 @@ __device__ __forceinline__ int ulp_exp(float x) {
 
 namespace vsim {
 
+// ------------------------------------------------------------------ sequential double sum
+// The reference's mean sum, s = ((0 + x0) + x1) + ... in double over a float row (ggml.c:
+// 4264-4270), by one wave without running the n dependent adds when it can prove the result:
+// chunks of 256 elements (4 per lane), and per chunk
+//  * a certificate that every partial sum of the chunk is exact in double (its elements are
+//    multiples of 2^umin and sum|x| < 2^(53+umin)), so the chunk's prefix sums P_j are exact
+//    in any order (a lane-local sum, then a wave scan);
+//  * speculation from the running value s at the chunk's position b: T_j = s + (P_j - P_b),
+//    each checked with TwoSum.  While every T_j is exact, each sequential add was exact and
+//    the sequential value after j elements is T_j; at the first j whose add rounds, the
+//    sequential value is RN(s + (P_j - P_b)) = T_j (the exact operand of that one rounding),
+//    and speculation restarts there.  A chunk that fails its certificate, or rounds more than
+//    CAP times, is added sequentially by lane 0 from where it stands.
+// Rows with one tiny element (why the whole-row certificate fails on ~3 % of rows) pass every
+// chunk certificate and speculate without a restart: 16 chunk steps instead of 4096 adds.
+__device__ __forceinline__ double rl_d(double v, int l) {  // lane l's v (l wave-uniform)
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFF), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __noinline__ double seq_sum_exact(const float *row, int n, int lane) {
+  constexpr int CAP = 32;
+  const int n4 = n / 4;
+  double s = 0.0;
+  for (int c4 = 0; c4 < n4; c4 += 64) {
+    const int i4 = c4 + lane;
+    const float4 v = i4 < n4 ? ((const float4 *)row)[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    int um = 1 << 30;
+    double sa = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      um = min(um, ulp_exp(e[k]));
+      sa += (double)fabsf(e[k]);
+    }
+    um = wave_min_i(um);
+    sa = wave_sum_d(sa);
+    const int cn = min(256, n - 4 * c4);  // elements in this chunk
+    int b = 0;                            // elements of the chunk already in s
+    if (um == (1 << 30) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um)) {
+      // exact prefix sums: p[k] = elements 0 .. 4 lane + k of the chunk
+      double p[4];
+      p[0] = e[0];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) p[k] = p[k - 1] + (double)e[k];
+      double x = p[3];  // inclusive scan of the lanes' sums
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const double t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+      }
+      const double ex = x - p[3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] += ex;
+      double pb = 0.0;  // P_b
+      for (int r = 0; r <= CAP; ++r) {
+        // first element position j (1-based within the chunk, j > b) whose add rounds
+        int jl = 1 << 30;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+          const int j = 4 * lane + k + 1;
+          if (j > b && j <= cn) {
+            const double d = p[k] - pb, t = s + d, bb = t - s, er = (s - (t - bb)) + (d - bb);
+            if (er != 0.0 || t != t) jl = j;
+          }
+        }
+        const int j = wave_min_i(jl);
+        if (j == (1 << 30)) {  // every remaining add exact (n % 4 == 0: the chunk ends on a lane's p[3])
+          s = s + (rl_d(p[3], (cn - 1) >> 2) - pb);
+          b = cn;
+          break;
+        }
+        const int kj = (j - 1) & 3;
+        const double pj = rl_d(kj == 0 ? p[0] : kj == 1 ? p[1] : kj == 2 ? p[2] : p[3], (j - 1) >> 2);
+        s = s + (pj - pb);  // the one rounding of step j
+        pb = pj;
+        b = j;
+      }
+    }
+    if (b < cn) {  // certificate failed or too many roundings: the rest of the chunk in order
+      double m = s;
+      if (lane == 0)
+        for (int j = b; j < cn; ++j) m += (double)row[4 * c4 + j];
+      s = rl_d(m, 0);
+    }
+  }
+  return s;
+}
+
 // ------------------------------------------------------------------ exact LayerNorm core
 // ggml_compute_forward_norm_f32 (ggml.c:4246-4304) for one row by one NT-thread block,
 // result left in `row` (LDS, n floats, in place).  The reference sums sequentially in
@@ -270,18 +360,12 @@ __device__ void ln_exact_lds_t(const float *__restrict__ x, float *row, int n, c
   }
   const bool exact = !CERT || (um == (1 << 30)) || sa * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + um);
   if (!exact) {
-    // sequential fallback, 4 independent partial loads per step to keep the LDS reads ahead
-    if (threadIdx.x == 0) {
-      double m = 0.0;
-      for (int i = 0; i < n4; ++i) {
-        const float4 v = ((const float4 *)row)[i];
-        m += v.x;
-        m += v.y;
-        m += v.z;
-        m += v.w;
+    if (wid == 0) {
+      const double m = seq_sum_exact(row, n, lane);
+      if (lane == 0) {
+        bcast_d = m;
+        if (stats) atomicAdd(&stats[0], 1u);
       }
-      bcast_d = m;
-      if (stats) atomicAdd(&stats[0], 1u);
     }
     __syncthreads();
     s = bcast_d;
