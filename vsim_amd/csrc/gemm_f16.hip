@@ -282,8 +282,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // this wave's LDS area (LDSB: the workgroup's LDS bytes, 8 waves), with the EM extra work.
 // The caller has passed a barrier after its last LDS operand read; a wave may call it again
 // for its next region (its own LDS writes and reads are ordered).
-template <bool GQ, int EM, int MW, int LDSB>
-__device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int mw, int nc0, int M, int N,
+template <bool GQ, int EM, int MW, int LDSB, int NC = 64>
+__device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][NC / 16], int mw, int nc0, int M, int N,
                                             const float *__restrict__ bias, float *__restrict__ Y,
                                             const uint16_t *__restrict__ gelu_tab, _Float16 *__restrict__ Q16,
                                             const G2Epi &epi, _Float16 *lds, int wave, int lane) {
@@ -294,7 +294,7 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int 
     constexpr int LDH = MW + 8;  // LDS row stride (halves, padded)
     _Float16 *eh = lds + wave * 32 * LDH;
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < NC / 32; ++pass) {
 #pragma unroll
     for (int p = 0; p < MW / 32; ++p) {
       const int mb = mw + 32 * p;  // the block's first row
@@ -347,20 +347,14 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int 
   constexpr int CP = 8 * 32 * LDW * 4 <= LDSB ? 32 : 16;  // columns per pass
   float *ep = (float *)lds + wave * CP * LDW;
   const bool vec = (M & 3) == 0;
-#pragma unroll
-  for (int pass = 0; pass < 64 / CP; ++pass) {
-#pragma unroll
-    for (int i = 0; i < MW / 16; ++i)
-#pragma unroll
-      for (int jj = 0; jj < CP / 16; ++jj)
-        *(f32x4 *)(ep + (16 * jj + fr) * LDW + 16 * i + 4 * fk) = acc[i][(CP / 16) * pass + jj];
-    // (a wave's own LDS writes and reads are ordered)
-    constexpr int RW = MW / 4, NIT = CP * RW / 64;  // float4 chunks per column run; per lane
-    static_assert(CP * RW % 64 == 0, "whole chunks per lane");
-    // the epilogue's extra inputs, all loaded before the pass's first store (Y may be epi.res,
-    // and a load behind a store it may alias waits for it: one exposed latency per chunk)
-    [[maybe_unused]] f32x4 xr[EM == 2 ? NIT : 1], xa[EM == 2 ? NIT : 1];
-    [[maybe_unused]] double2 cq[EM == 1 ? NIT : 1][2];
+  constexpr int RW = MW / 4, NIT = CP * RW / 64;  // float4 chunks per column run; per lane
+  static_assert(CP * RW % 64 == 0, "whole chunks per lane");
+  // the epilogue's extra inputs, software-pipelined one pass ahead: pass p+1's are issued
+  // before pass p's stores (Y may be epi.res, and a load behind a store it may alias waits for
+  // it; pass p+1's columns are not pass p's), so only the first pass's latency is exposed
+  [[maybe_unused]] f32x4 xr[2][EM == 2 ? NIT : 1], xa[2][EM == 2 ? NIT : 1];
+  [[maybe_unused]] double2 cq[2][EM == 1 ? NIT : 1][2];
+  auto extra = [&](int pass, int slot) {
     if constexpr (EM != 0) {
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
@@ -368,17 +362,30 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int 
         const int n = nc0 + CP * pass + nl, m = mw + 4 * c;
         if (n >= N || m >= M) continue;
         if constexpr (EM == 2) {
-          xr[it] = *(const f32x4 *)(epi.res + (size_t)n * M + m);
-          if (epi.res_a) xa[it] = *(const f32x4 *)(epi.res_a + (size_t)n * M + m);
+          xr[slot][it] = *(const f32x4 *)(epi.res + (size_t)n * M + m);
+          if (epi.res_a) xa[slot][it] = *(const f32x4 *)(epi.res_a + (size_t)n * M + m);
         } else {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int dd = (m + 2 * q) % epi.d;
-            cq[it][q] = dd < epi.n_rot ? epi.cs[(size_t)(epi.p0 + n) * (epi.n_rot / 2) + dd / 2] : make_double2(1.0, 0.0);
+            cq[slot][it][q] =
+                dd < epi.n_rot ? epi.cs[(size_t)(epi.p0 + n) * (epi.n_rot / 2) + dd / 2] : make_double2(1.0, 0.0);
           }
         }
       }
     }
+  };
+  extra(0, 0);
+#pragma unroll
+  for (int pass = 0; pass < NC / CP; ++pass) {
+    const int sl = pass & 1;
+    if (pass + 1 < NC / CP) extra(pass + 1, sl ^ 1);
+#pragma unroll
+    for (int i = 0; i < MW / 16; ++i)
+#pragma unroll
+      for (int jj = 0; jj < CP / 16; ++jj)
+        *(f32x4 *)(ep + (16 * jj + fr) * LDW + 16 * i + 4 * fk) = acc[i][(CP / 16) * pass + jj];
+    // (a wave's own LDS writes and reads are ordered)
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int idx = lane + 64 * it, nl = idx / RW, c = idx % RW;
@@ -393,7 +400,7 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int 
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if ((m + 2 * q) % epi.d < epi.n_rot) {
-            const double2 cs = cq[it][q];
+            const double2 cs = cq[sl][it][q];
             const double x0 = v[2 * q], x1 = v[2 * q + 1];
             v[2 * q] = (float)(x0 * cs.x - x1 * cs.y);
             v[2 * q + 1] = (float)(x0 * cs.y + x1 * cs.x);
@@ -408,10 +415,10 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][4], int 
       if constexpr (EM == 2) {
         if (epi.res_a) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = xr[it][e] + (xa[it][e] + v[e]);
+          for (int e = 0; e < 4; ++e) v[e] = xr[sl][it][e] + (xa[sl][it][e] + v[e]);
         } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] + xr[it][e];
+          for (int e = 0; e < 4; ++e) v[e] = v[e] + xr[sl][it][e];
         }
       }
       float *dst = Y + (size_t)n * M + m;
@@ -773,17 +780,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
   if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped loads past the end have landed
   __syncthreads();
-  // the wave's 32 rows x 256 columns as four 32 x 64 regions
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f32x4 aq[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) aq[i][j] = acc[i][4 * q + j];
-    g2_epilogue<GQ, EM, 32, r_lds_bytes()>(aq, m0 + 32 * wave, n0 + 64 * q, M, N, bias, Y, gelu_tab, Q16, epi, g2lds,
-                                           wave, lane);
-  }
+  // the wave's 32 rows x 256 columns
+  g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 + 32 * wave, n0, M, N, bias, Y, gelu_tab, Q16, epi, g2lds, wave,
+                                              lane);
 }
 
 template <bool GQ, int EM>
