@@ -187,6 +187,11 @@ int vsim_op_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, i
  * out[q][h*d + dd] = softmax_k(scale * K.Q, causal) . V.  d in {64, 96, 128, 256}. */
 int vsim_op_attn_prefill(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
                          float scale, float *out, void *stream);
+/* The same attention (d = 256 only) written as the next GEMM's fp16 operand out16 [N][d*H]:
+ * quantize_row_q4_0 (ggml.c:209-251) of each 32-value block of the output row, the values
+ * d*(q-8) as fp16 -- what vsim_op_act_quant_f16 makes of vsim_op_attn_prefill's out. */
+int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
+                             float scale, void *out16, void *stream);
 /* device fp16 tables (exp, gelu) as built by ggml_init (ggml.c:1240-1251) */
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host);
 

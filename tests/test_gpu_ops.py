@@ -511,6 +511,28 @@ def test_prefill_gemm_q4_in_lds_dequant_bit_identical(M, K, N):
                                              None), init=R)
 
 
+@pytest.mark.parametrize("H,N,n_past", [(2, 200, 0), (3, 300, 37), (1, 64, 130)])
+def test_attn_prefill_quantized_output_bit_identical(H, N, n_past):
+    """d = 256: the attention writing the out-projection's fp16 operand itself
+    (vsim_op_attn_prefill_q16) gives the bits vsim_op_act_quant_f16 makes of its f32 output."""
+    d = 256
+    rng = np.random.default_rng(7 * N + n_past)
+    E, nk = d * H, n_past + N
+    q_, k_, v_ = (dev(rng.standard_normal((n, E)).astype(np.float32)) for n in (N, nk, nk))
+    scale = float(np.float32(1.0 / np.sqrt(d)))
+    L = hip.lib()
+    out = torch.empty(N * E, dtype=torch.float32, device=DEV)
+    hip.check(L.vsim_op_attn_prefill(q_.data_ptr(), k_.data_ptr(), v_.data_ptr(), d, H, N, n_past, scale,
+                                     out.data_ptr(), None), "attn")
+    ref16 = torch.empty(N * E, dtype=torch.float16, device=DEV)
+    hip.check(L.vsim_op_act_quant_f16(out.data_ptr(), E, N, None, 0, ref16.data_ptr(), None), "act_quant")
+    got16 = torch.full((N * E,), float("nan"), dtype=torch.float16, device=DEV)
+    hip.check(L.vsim_op_attn_prefill_q16(q_.data_ptr(), k_.data_ptr(), v_.data_ptr(), d, H, N, n_past, scale,
+                                         got16.data_ptr(), None), "attn_q16")
+    torch.cuda.synchronize()
+    assert torch.equal(got16.view(torch.int16), ref16.view(torch.int16))
+
+
 @pytest.mark.parametrize("d,H,N,n_past", [(256, 2, 200, 0), (256, 3, 300, 37), (256, 1, 64, 130), (256, 2, 1100, 40),
                                            (128, 3, 130, 17), (96, 2, 64, 5), (64, 4, 9, 40)])
 def test_attn_prefill_f16(d, H, N, n_past):

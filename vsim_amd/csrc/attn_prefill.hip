@@ -317,7 +317,8 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
                                                                        const _Float16 *__restrict__ k16,
                                                                        const _Float16 *__restrict__ vt16, int E, int H,
                                                                        int N, int n_past, int ldt, float qscale,
-                                                                       float *__restrict__ out) {
+                                                                       float *__restrict__ out,
+                                                                       _Float16 *__restrict__ out16) {
   constexpr int D = 256;
   extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
   // [0, 128 KB): K and V^T tiles, two buffers each (as k_attn_prefill_f16's D = 256 path);
@@ -454,8 +455,37 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
   mex[(grp * 2 + half) * 64 + lane] = lrow;
   __syncthreads();
   const float lt = mex[(grp * 2) * 64 + lane] + mex[(grp * 2 + 1) * 64 + lane];
+  const float inv = 1.0f / lt;
+  if (out16) {
+    // the wo GEMM's fp16 operand straight from here: quantize_row_q4_0 per 32 dims of the
+    // query's row, the values d*(q-8) as fp16 -- k_act_quant_f16's arithmetic on the same f32
+    // values (dims 32 i .. 32 i + 31 of this half: 16 in this lane, 16 in lane ^ 32)
+    _Float16 *qrow = out16 + (size_t)min(myq, N - 1) * E + h * D + 128 * half;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[16], amax = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        v[k] = o[i][k] * inv;
+        amax = amax > fabsf(v[k]) ? amax : fabsf(v[k]);
+      }
+      const float ao = __shfl_xor(amax, 32, 64);
+      amax = amax > ao ? amax : ao;
+      const float d = amax / 7.0f;
+      const float id = d != 0.0f ? 1.0f / d : 0.0f;
+      if (myq < N) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          ahalf4 hq;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hq[e] = f16_of_product(d, (float)x86_round_i8(v[4 * g + e] * id));
+          *(ahalf4 *)(qrow + 32 * i + 8 * g + 4 * hl) = hq;
+        }
+      }
+    }
+    return;
+  }
   if (myq < N) {
-    const float inv = 1.0f / lt;
     float *orow = out + (size_t)myq * E + h * D + 128 * half;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -469,6 +499,13 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
 }
 
 bool attn_prefill_supported(int d) { return d == 64 || d == 96 || d == 128 || d == 256; }
+#ifndef VSIM_ATTN_PAIR  // (A/B builds: 0 keeps D = 256 on the one-wave-per-group kernel)
+#define VSIM_ATTN_PAIR 1
+#endif
+#ifndef VSIM_ATTN_Q16  // 0: the out-projection's fp16 operand made by a separate quantization pass (A/B)
+#define VSIM_ATTN_Q16 1
+#endif
+bool attn_prefill_quantizes(int d) { return VSIM_ATTN_PAIR && VSIM_ATTN_Q16 && d == 256; }
 
 template <int D>
 size_t attn_prefill_lds() {
@@ -483,9 +520,14 @@ _Float16 *attn_prefill_vt16(void *scratch, int E, int nk) {
 }
 
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
-                            float scale, float *out, hipStream_t s, void *scratch, size_t scratch_bytes, bool fresh) {
+                            float scale, float *out, hipStream_t s, void *scratch, size_t scratch_bytes, bool fresh,
+                            void *out16) {
   if (!attn_prefill_supported(d)) {
     set_error("attention prefill: head dim must be 64, 96, 128 or 256");
+    return VSIM_EINVAL;
+  }
+  if (out16 && !attn_prefill_quantizes(d)) {
+    set_error("attention prefill: the quantized fp16 output needs head dim 256");
     return VSIM_EINVAL;
   }
   const int E = d * H, nk = n_past + N;
@@ -514,9 +556,6 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
                                  (int)attn_prefill_lds<256>()));
     attr = true;
   }
-#ifndef VSIM_ATTN_PAIR  // (A/B builds: 0 keeps D = 256 on the one-wave-per-group kernel)
-#define VSIM_ATTN_PAIR 1
-#endif
   if (VSIM_ATTN_PAIR && d == 256) {
     static bool attr2 = false;
     if (!attr2) {
@@ -525,7 +564,7 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
       attr2 = true;
     }
     hipLaunchKernelGGL(k_attn_prefill_pair, grid, dim3(AP2_THREADS), ap2_lds(), s, Q, k16, vt16, E, H, N, n_past, ldt,
-                       qscale, out);
+                       qscale, out, (_Float16 *)out16);
     VSIM_HIP(hipGetLastError());
     if (own) VSIM_HIP(hipFreeAsync(buf, s));
     return VSIM_OK;

@@ -147,6 +147,11 @@ int vsim_op_attn_prefill(const float *Q, const float *kc, const float *vc, int d
                          float scale, float *out, void *stream) {
   return launch_attn_prefill_f16(Q, kc, vc, d, H, N, n_past, scale, out, (hipStream_t)stream);
 }
+int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
+                             float scale, void *out16, void *stream) {
+  return launch_attn_prefill_f16(Q, kc, vc, d, H, N, n_past, scale, nullptr, (hipStream_t)stream, nullptr, 0, false,
+                                 out16);
+}
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host) { return tables_host(exp_f16_host, gelu_f16_host); }
 
 }  // extern "C"

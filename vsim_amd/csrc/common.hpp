@@ -170,6 +170,16 @@ __device__ __forceinline__ int x86_round_i8(float v) {
   return (int)(int8_t)i;
 }
 
+// The prompt GEMMs' fp16 activation value d*(q-8): the exact f32 x f32 product rounded once to
+// fp16 (v_fma_mix with addend +0; d >= 0, so the product is never -0).  Spelled out because the
+// compiler folds fptrunc(fmul) into this instruction in some kernels and rounds twice (f32,
+// then fp16) in others -- and every producer of that operand must give the same bits.
+__device__ __forceinline__ _Float16 f16_of_product(float a, float b) {
+  uint32_t r;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return __builtin_bit_cast(_Float16, (uint16_t)r);
+}
+
 // ---------------------------------------------------------------- wave reductions
 // Butterfly/broadcast steps in DPP (a few cycles each instead of an LDS permute round trip):
 // quad_perm xor 1 and 2, row_half_mirror (8), row_mirror (16), row_bcast15 and row_bcast31
@@ -298,9 +308,12 @@ bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call); fresh: the new keys [n_past, n_past + N) are
 // already there (written by the K and V GEMM epilogues, attn_prefill_k16/_vt16 give where)
+// out16 (head dim 256 only, attn_prefill_quantizes): instead of out, the next GEMM's fp16
+// operand -- quantize_row_q4_0 of each 32-value block, d*(q-8) as fp16 (k_act_quant_f16's values)
 int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
                             float scale, float *out, hipStream_t s, void *scratch = nullptr, size_t scratch_bytes = 0,
-                            bool fresh = false);
+                            bool fresh = false, void *out16 = nullptr);
+bool attn_prefill_quantizes(int d);
 int attn_prefill_ldt(int nk);  // V^T row length (keys padded to the key tile)
 _Float16 *attn_prefill_k16(void *scratch, int E, int nk);
 _Float16 *attn_prefill_vt16(void *scratch, int E, int nk);

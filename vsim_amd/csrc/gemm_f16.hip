@@ -60,8 +60,8 @@ __device__ __forceinline__ void deq_block_f16(uint4 q, float d, half8 out[4]) {
 }
 
 // The activation rows dequantized once per GEMM call: X16[token][K], block i = token * nb + b
-// at X16 + 32 i, each value (fp16)(d * (q - 8)) with the f32 product rounded first -- the
-// halves k_act_quant_f16 writes (activations round twice, the weights once: deq_word_f16).
+// at X16 + 32 i, each value d * (q - 8) rounded once to fp16 (f16_of_product) -- the halves
+// k_act_quant_f16 writes.
 __global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__ xqs, const float *__restrict__ xdd,
                                                       size_t nblk, half8 *__restrict__ X16) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -74,11 +74,8 @@ __global__ void __launch_bounds__(256) k_act_deq_f16(const uint8_t *__restrict__
     half8 h;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float p0 = d * (float)((int)((qw[w] >> (8 * j)) & 15u) - 8);
-      float p1 = d * (float)((int)((qw[w] >> (8 * j + 4)) & 15u) - 8);
-      asm volatile("" : "+v"(p0), "+v"(p1));  // (kept apart from the conversion: two roundings)
-      h[2 * j] = (_Float16)p0;
-      h[2 * j + 1] = (_Float16)p1;
+      h[2 * j] = f16_of_product(d, (float)((int)((qw[w] >> (8 * j)) & 15u) - 8));
+      h[2 * j + 1] = f16_of_product(d, (float)((int)((qw[w] >> (8 * j + 4)) & 15u) - 8));
     }
     X16[4 * i + w] = h;
   }
@@ -114,7 +111,7 @@ __global__ void __launch_bounds__(256) k_act_quant_f16(const float *__restrict__
     }
     float d;
     const int q = q4_half(t, d);
-    if (ok) X16[blk * QK + (lane & 31)] = (_Float16)(d * (float)(q - 8));
+    if (ok) X16[blk * QK + (lane & 31)] = f16_of_product(d, (float)(q - 8));
   }
 }
 
@@ -323,7 +320,7 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][NC / 16]
         const float id = d != 0.0f ? 1.0f / d : 0.0f;
         _Float16 h[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) h[e] = (_Float16)(d * (float)(x86_round_i8(v[e] * id)));
+        for (int e = 0; e < 8; ++e) h[e] = f16_of_product(d, (float)x86_round_i8(v[e] * id));
         _Float16 *row = eh + ((j & 1) * 16 + fr) * LDH + 32 * p + 4 * fk;
         *(uint2 *)row = *(const uint2 *)&h[0];
         *(uint2 *)(row + 16) = *(const uint2 *)&h[4];

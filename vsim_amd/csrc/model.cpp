@@ -643,17 +643,19 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
   // attention (vsim.cpp:583-616)
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
+  // (head dim 256: the attention writes the out-projection's fp16 operand itself)
+  const bool attn_q16 = attn16 && pf && attn_prefill_quantizes(d);
   if (attn16) {
     // fast-mode prompt: one-pass fp16 MFMA attention (attn_prefill.hip)
     RC(launch_attn_prefill_f16(m->Qb, kc, vc, d, H, N, n_past, scale, m->attn_in, s, m->pf_scratch, m->pf_bytes,
-                               kv16_epi));
+                               kv16_epi, attn_q16 ? X.b : nullptr));
     nk += 2;
   } else {
     RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
     RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
     RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
   }
-  RC(act16(m->attn_in, E, X.b, nullptr, false));
+  if (!attn_q16) RC(act16(m->attn_in, E, X.b, nullptr, false));
   RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, gptj ? nullptr : L.bo, m->attn, nk, X.b));
   // feed-forward input
   const uint8_t *fxq = m->xq1;

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(NORMQ_THREADS) k_norm_f16q(const float *__rest
     const float v = ok ? xrow[b * QK + (lane & 31)] : 0.0f;
     float d;
     const int qv = q4_half(v, d);
-    if (ok) q[b * QK + (lane & 31)] = (_Float16)(d * (float)(qv - 8));
+    if (ok) q[b * QK + (lane & 31)] = f16_of_product(d, (float)(qv - 8));
   }
 }
 
