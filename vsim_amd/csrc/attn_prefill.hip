@@ -61,14 +61,14 @@ __global__ void __launch_bounds__(256) k_kv_f16(const float *__restrict__ kc, co
     const int cc = e / 16, k4 = (e % 16) * 4;
     const int col = col0 + cc, h = col / d, dim = col % d;
     ahalf4 hv = {(_Float16)tv[k4][cc], (_Float16)tv[k4 + 1][cc], (_Float16)tv[k4 + 2][cc], (_Float16)tv[k4 + 3][cc]};
-    _Float16 *dst = vt16 + ((size_t)h * d + dim) * ldt + key0 + k4;
+    _Float16 *dst = vt16 + ((size_t)h * d + dim) * ldt;  // (keys in vt_pos order: a quad stays whole)
     const int k = key0 + k4;
     if (k + 4 <= f0 || k >= f1) {
-      if (k < ldt) *(ahalf4 *)dst = hv;
+      if (k < ldt) *(ahalf4 *)(dst + vt_pos(k)) = hv;
     } else {  // (a group that straddles the fresh range)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if ((k + j < f0 || k + j >= f1) && k + j < ldt) dst[j] = hv[j];
+        if ((k + j < f0 || k + j >= f1) && k + j < ldt) dst[vt_pos(k + j)] = hv[j];
     }
   }
 }
@@ -268,10 +268,9 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 #pragma unroll
           for (int i = 0; i < NT; ++i) {
             const int vrow = 32 * i + r, vc = kbase2 >> 3;  // (kbase2 & 7 == 4 hl: within the chunk)
-            const _Float16 *vr = GL ? &Vt[vrow * AP_BK + 8 * (vc ^ ((vrow >> 1) & 7)) + 4 * hl] : &Vt[vrow * VLD + kbase2];
-            const _Float16 *vr1 = GL ? &Vt[vrow * AP_BK + 8 * ((vc + 1) ^ ((vrow >> 1) & 7)) + 4 * hl] : vr + 8;
-            const ahalf4 v0 = *(const ahalf4 *)vr, v1 = *(const ahalf4 *)vr1;
-            const ahalf8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            // (vt_pos order: the lane's keys kbase2 .. +3 and kbase2 + 8 .. +11 are chunk vc + hl)
+            const ahalf8 vf = GL ? *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * ((vc + hl) ^ ((vrow >> 1) & 7))]
+                                 : *(const ahalf8 *)&Vt[vrow * VLD + 8 * (vc + hl)];
             o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
             if (D >= 256 && (i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
           }
@@ -310,6 +309,9 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 // Each wave keeps the running sum of its own keys' probabilities; the two partial sums are
 // added (half 0's first) at the end.  ≈190 registers: two waves per SIMD.  Barriers per key
 // block: after the maxima, after the P^T stores, after the next tile's DMA (as above).
+#ifndef VSIM_AP_ABL  // (timing-only ablation builds: 1 no tile loads, 2 no S MFMAs, 4 no PV MFMAs,
+#define VSIM_AP_ABL 0  //  8 no exponentials, 16 no wait for the next tile)
+#endif
 constexpr int AP2_THREADS = 512;
 constexpr size_t ap2_lds() { return (size_t)2 * 2 * AP_BK * 256 * sizeof(_Float16) + 4 * 2 * 2 * 64 * 16 + 4 * 2 * 64 * 4; }
 
@@ -380,7 +382,7 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * AP_BK, buf = kb & 1;
-    if (kb + 1 < nkb) gl_stage(kb + 1, buf ^ 1);
+    if (!(VSIM_AP_ABL & 1) && kb + 1 < nkb) gl_stage(kb + 1, buf ^ 1);
     const _Float16 *Ks = lds + buf * AP_BK * D;
     const _Float16 *Vt = lds + 2 * AP_BK * D + buf * D * AP_BK;
     const bool vis = k0 <= n_past + min(qw + 31, N - 1);  // uniform over the pair
@@ -390,7 +392,8 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
       for (int s = 0; s < D / 16; ++s) {
         const int krow = 32 * half + r;
         const ahalf8 kf = *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))];
-        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st, 0, 0, 0);
+        if (!(VSIM_AP_ABL & 2)) st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st, 0, 0, 0);
+        else st[s] += (float)kf[0];
         if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       float bm = -INFINITY;
@@ -410,7 +413,7 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
       float ls = 0.0f;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const float pv = st[g] == -INFINITY ? 0.0f : exp2f(st[g] - mnew);
+        const float pv = (VSIM_AP_ABL & 8) ? st[g] : st[g] == -INFINITY ? 0.0f : exp2f(st[g] - mnew);
         st[g] = pv;
         ls += pv;
       }
@@ -440,15 +443,13 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int vrow = 128 * half + 32 * i + r, vc = kbase2 >> 3;
-            const _Float16 *vr = &Vt[vrow * AP_BK + 8 * (vc ^ ((vrow >> 1) & 7)) + 4 * hl];
-            const _Float16 *vr1 = &Vt[vrow * AP_BK + 8 * ((vc + 1) ^ ((vrow >> 1) & 7)) + 4 * hl];
-            const ahalf4 v0 = *(const ahalf4 *)vr, v1 = *(const ahalf4 *)vr1;
-            const ahalf8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-            o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
+            const ahalf8 vf = *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * ((vc + hl) ^ ((vrow >> 1) & 7))];
+            if (!(VSIM_AP_ABL & 4)) o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
+            else o[i][0] += (float)vf[0] + (float)pf[1];
           }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile has landed
+    if (!(VSIM_AP_ABL & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile has landed
     __syncthreads();
   }
   // the running sums of both halves (half 0's + half 1's, in that order, in both waves)

@@ -290,7 +290,13 @@ int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
 //    y may be res);
 //  * h16 != null (with or without RoPE): the result also as fp16 for the prompt attention,
 //    row-major at h16[(p0 + n) * M + m] (its K copy), or with h16_t, transposed at
-//    h16[m * h16_ld + p0 + n] (its V^T copy) -- what k_kv_f16 makes of the cache rows.
+//    h16[m * h16_ld + vt_pos(p0 + n)] (its V^T copy) -- what k_kv_f16 makes of the cache rows.
+// Key order of the prompt attention's V^T copy within each 16-key group: keys 0-3, 8-11,
+// 4-7, 12-15 (the middle quads swapped), so the 8 keys one lane of the P^T MFMA operand needs
+// (4 hl .. 4 hl + 3 and 8 + 4 hl .. 11 + 4 hl, the S^T accumulator's row order) are 16
+// contiguous bytes: one ds_read_b128 per V fragment, conflict-free under the tile's swizzle.
+__host__ __device__ constexpr int vt_pos(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
+
 struct G2Epi {
   const double2 *cs = nullptr;
   int d = 0, n_rot = 0, p0 = 0;

@@ -441,13 +441,16 @@ __device__ __forceinline__ void g2_epilogue(const f32x4 (&acc)[MW / 16][NC / 16]
         half8 h;
 #pragma unroll
         for (int j = 0; j < 8; ++j) h[j] = (_Float16)(ep[(8 * c8 + j) * LDW + ml] + bm);
-        _Float16 *dst = epi.h16 + (size_t)m * epi.h16_ld + epi.p0 + nb;
-        if (nb + 8 <= N && ((epi.p0 + nb) & 7) == 0) {
-          *(half8 *)dst = h;
+        _Float16 *dst = epi.h16 + (size_t)m * epi.h16_ld;
+        const int k = epi.p0 + nb;  // (keys in vt_pos order: an aligned run of 8 is two quads)
+        if (nb + 8 <= N && (k & 7) == 0) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          *(h4 *)(dst + vt_pos(k)) = (h4){h[0], h[1], h[2], h[3]};
+          *(h4 *)(dst + vt_pos(k + 4)) = (h4){h[4], h[5], h[6], h[7]};
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (nb + j < N) dst[j] = h[j];
+            if (nb + j < N) dst[vt_pos(k + j)] = h[j];
         }
       }
     }
