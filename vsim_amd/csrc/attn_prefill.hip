@@ -309,8 +309,8 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 // Each wave keeps the running sum of its own keys' probabilities; the two partial sums are
 // added (half 0's first) at the end.  ≈190 registers: two waves per SIMD.  Barriers per key
 // block: after the maxima, after the P^T stores, after the next tile's DMA (as above).
-#ifndef VSIM_AP_ABL  // (timing-only ablation builds: 1 no tile loads, 2 no S MFMAs, 4 no PV MFMAs,
-#define VSIM_AP_ABL 0  //  8 no exponentials, 16 no wait for the next tile)
+#ifndef VSIM_AP_STAGGER  // (A/B builds: 0 runs both wave groups in the same phase)
+#define VSIM_AP_STAGGER 1
 #endif
 constexpr int AP2_THREADS = 512;
 constexpr size_t ap2_lds() { return (size_t)2 * 2 * AP_BK * 256 * sizeof(_Float16) + 4 * 2 * 2 * 64 * 16 + 4 * 2 * 64 * 4; }
@@ -330,7 +330,11 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
   const int nqb = (N + AP_BQ - 1) / AP_BQ;
   const int h = blockIdx.x % H, q0 = (nqb - 1 - (int)blockIdx.x / H) * AP_BQ;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wv & 3, half = wv >> 2;
+  // pair (2 g, 2 g + 1) takes query group g; groups 0, 1 (waves 0-3, one per SIMD) lead, groups
+  // 2, 3 (waves 4-7) run one barrier behind (VSIM_AP_STAGGER), so the two waves on a SIMD are
+  // in different phases: one's softmax beside the other's MFMAs
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wv >> 1, half = wv & 1;
+  const bool lag = VSIM_AP_STAGGER && wv >= 4;
   const int r = lane & 31, hl = lane >> 5;
   const int qw = q0 + grp * 32;
   const int myq = qw + r;
@@ -360,40 +364,54 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
   const int klast = n_past + min(q0 + AP_BQ, N) - 1;
   const int nkb = klast / AP_BK + 1;
   const uint32_t lb = lds_addr(lds);
-  auto gl_stage = [&](int kb, int buf) __attribute__((always_inline)) {
-    const int k0 = kb * AP_BK;
+  // K(kb) into K buffer kb & 1, V^T(kb) into V buffer kb & 1: each wave 4 LDS-DMAs per tile
+  auto stage_k = [&](int kb) __attribute__((always_inline)) {
+    const int k0 = kb * AP_BK, buf = kb & 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // K: 2 rows (keys) per wave instruction
+    for (int j = 0; j < 4; ++j) {  // 2 rows (keys) per wave instruction
       const int row0 = (j * 8 + wv) * 2, row = row0 + (lane >> 5);
       const int c = (lane & 31) ^ (row & 15);
       glds16<false>(kbase + (size_t)min(k0 + row, klast) * E + 8 * c,
                     lb + (uint32_t)((buf * AP_BK * D + row0 * D) * 2));
     }
+  };
+  auto stage_v = [&](int kb) __attribute__((always_inline)) {
+    const int k0 = kb * AP_BK, buf = kb & 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // V^T: 8 rows (dims) per wave instruction
+    for (int j = 0; j < 4; ++j) {  // 8 rows (dims) per wave instruction
       const int row0 = (j * 8 + wv) * 8, row = row0 + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       glds16<false>(vbase + (size_t)row * ldt + k0 + 8 * c,
                     lb + (uint32_t)((2 * AP_BK * D + buf * D * AP_BK + row0 * AP_BK) * 2));
     }
   };
-  gl_stage(0, 0);
+  // Tiles 0 and 1 up front; then K(kb+2) is issued at the start of PV(kb) (its buffer's last
+  // reader is S(kb), one phase earlier even for the lagging group) and waited for at the end of
+  // SM(kb+1); V(kb+1) at the start of SM(kb) (last reader PV(kb-1)), waited for at the end of
+  // S(kb+1).  In issue order V(kb+1) follows K(kb+1) and K(kb+2) follows V(kb+1), so each wait
+  // leaves the one later tile (4 DMAs) in flight.
+  stage_k(0);
+  stage_v(0);
+  if (nkb > 1) {
+    stage_k(1);
+    stage_v(1);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (lag) __builtin_amdgcn_s_barrier();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * AP_BK, buf = kb & 1;
-    if (!(VSIM_AP_ABL & 1) && kb + 1 < nkb) gl_stage(kb + 1, buf ^ 1);
     const _Float16 *Ks = lds + buf * AP_BK * D;
     const _Float16 *Vt = lds + 2 * AP_BK * D + buf * D * AP_BK;
     const bool vis = k0 <= n_past + min(qw + 31, N - 1);  // uniform over the pair
+    // ---- S(kb): S^T of this wave's 32 keys, the block maximum to the partner
     af32x16 st = (af32x16){};
     if (vis) {
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
         const int krow = 32 * half + r;
         const ahalf8 kf = *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))];
-        if (!(VSIM_AP_ABL & 2)) st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st, 0, 0, 0);
-        else st[s] += (float)kf[0];
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st, 0, 0, 0);
         if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       float bm = -INFINITY;
@@ -406,14 +424,22 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
       mex[(grp * 2 + half) * 64 + lane] = bm;
     }
+    if (kb >= 2) {  // this wave's V(kb) DMAs
+      if (kb + 1 < nkb)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
+    // ---- SM(kb): the pair's common maximum, P^T of this wave's keys to the partner
+    if (kb >= 1 && kb + 1 < nkb) stage_v(kb + 1);
     if (vis) {
       const float mnew = fmaxf(mrow, fmaxf(mex[(grp * 2) * 64 + lane], mex[(grp * 2 + 1) * 64 + lane]));
       const float alpha = mnew == -INFINITY ? 1.0f : exp2f(mrow - mnew);
       float ls = 0.0f;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const float pv = (VSIM_AP_ABL & 8) ? st[g] : st[g] == -INFINITY ? 0.0f : exp2f(st[g] - mnew);
+        const float pv = st[g] == -INFINITY ? 0.0f : exp2f(st[g] - mnew);
         st[g] = pv;
         ls += pv;
       }
@@ -430,28 +456,29 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
         pex[((grp * 2 + half) * 2 + s2) * 64 + lane] = *(const u32x4 *)&pf;
       }
     }
+    if (kb >= 1 && kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this wave's K(kb+1) DMAs
     __syncthreads();
+    // ---- PV(kb): O^T dims 128 half + 32 i, keys 32 t + 16 s2 + ...: P^T of tile t from wave half t
+    if (kb + 2 < nkb) stage_k(kb + 2);
     if (vis) {
-      // O^T dims 128 half + 32 i, keys 32 t + 16 s2 + ...: P^T of tile t from wave half t
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const u32x4 pw = pex[((grp * 2 + t) * 2 + s2) * 64 + lane];
           const ahalf8 pf = *(const ahalf8 *)&pw;
-          const int kbase2 = 32 * t + 16 * s2 + 4 * hl;
+          const int vc = 4 * t + 2 * s2 + hl;  // (vt_pos order: the lane's 8 keys are one chunk)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int vrow = 128 * half + 32 * i + r, vc = kbase2 >> 3;
-            const ahalf8 vf = *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * ((vc + hl) ^ ((vrow >> 1) & 7))];
-            if (!(VSIM_AP_ABL & 4)) o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
-            else o[i][0] += (float)vf[0] + (float)pf[1];
+            const int vrow = 128 * half + 32 * i + r;
+            const ahalf8 vf = *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * (vc ^ ((vrow >> 1) & 7))];
+            o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
           }
         }
     }
-    if (!(VSIM_AP_ABL & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile has landed
     __syncthreads();
   }
+  if (VSIM_AP_STAGGER && !lag) __builtin_amdgcn_s_barrier();  // (pairs with the lagging group's last)
   // the running sums of both halves (half 0's + half 1's, in that order, in both waves)
   mex[(grp * 2 + half) * 64 + lane] = lrow;
   __syncthreads();
