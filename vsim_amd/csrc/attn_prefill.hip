@@ -309,6 +309,9 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 // Each wave keeps the running sum of its own keys' probabilities; the two partial sums are
 // added (half 0's first) at the end.  ≈190 registers: two waves per SIMD.  Barriers per key
 // block: after the maxima, after the P^T stores, after the next tile's DMA (as above).
+#ifndef AP_KPF  // K fragments in flight in the S^T chain (A/B builds)
+#define AP_KPF 4
+#endif
 #ifndef VSIM_AP_STAGGER  // (A/B builds: 0 runs both wave groups in the same phase)
 #define VSIM_AP_STAGGER 1
 #endif
@@ -407,12 +410,18 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
     // ---- S(kb): S^T of this wave's 32 keys, the block maximum to the partner
     af32x16 st = (af32x16){};
     if (vis) {
+      // K fragments AP_KPF steps ahead of their MFMA (LDS latency behind the chain)
+      const int krow = 32 * half + r;
+      auto kfrag = [&](int s) { return *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))]; };
+      ahalf8 kf[AP_KPF];
+#pragma unroll
+      for (int s = 0; s < AP_KPF; ++s) kf[s] = kfrag(s);
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
-        const int krow = 32 * half + r;
-        const ahalf8 kf = *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))];
-        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st, 0, 0, 0);
-        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s % AP_KPF], qf[s], st, 0, 0, 0);
+        if (s + AP_KPF < D / 16) kf[s % AP_KPF] = kfrag(s + AP_KPF);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
       }
       float bm = -INFINITY;
 #pragma unroll
@@ -461,20 +470,31 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
     // ---- PV(kb): O^T dims 128 half + 32 i, keys 32 t + 16 s2 + ...: P^T of tile t from wave half t
     if (kb + 2 < nkb) stage_k(kb + 2);
     if (vis) {
+      // step u = 2 t + s2 (16 keys): P^T from wave half t, V fragments of the 4 dim tiles;
+      // step u + 1's operands load while step u's 4 MFMAs run
+      auto pfrag = [&](int u) {
+        const u32x4 pw = pex[((grp * 2 + (u >> 1)) * 2 + (u & 1)) * 64 + lane];
+        return *(const ahalf8 *)&pw;
+      };
+      auto vfrag = [&](int u, int i) {  // (vt_pos order: the lane's 8 keys are chunk 2 u + hl)
+        const int vrow = 128 * half + 32 * i + r;
+        return *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * ((2 * u + hl) ^ ((vrow >> 1) & 7))];
+      };
+      ahalf8 pf[2], vf[2][4];
+      pf[0] = pfrag(0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int i = 0; i < 4; ++i) vf[0][i] = vfrag(0, i);
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const u32x4 pw = pex[((grp * 2 + t) * 2 + s2) * 64 + lane];
-          const ahalf8 pf = *(const ahalf8 *)&pw;
-          const int vc = 4 * t + 2 * s2 + hl;  // (vt_pos order: the lane's 8 keys are one chunk)
+      for (int u = 0; u < 4; ++u) {
+        if (u + 1 < 4) {
+          pf[(u + 1) & 1] = pfrag(u + 1);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int vrow = 128 * half + 32 * i + r;
-            const ahalf8 vf = *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * (vc ^ ((vrow >> 1) & 7))];
-            o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
-          }
+          for (int i = 0; i < 4; ++i) vf[(u + 1) & 1][i] = vfrag(u + 1, i);
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf[u & 1][i], pf[u & 1], o[i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     __syncthreads();
   }
