@@ -14,6 +14,9 @@ from vsim_amd import modelgen as mg  # noqa: E402
 
 N = int(os.environ.get("GEMM_N", "2048"))
 shapes = [(6144, 6144), (24576, 6144), (6144, 24576)]
+if os.environ.get("GEMM_SHAPES"):  # "M1xK1,M2xK2,..."
+    shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["GEMM_SHAPES"].split(",")]
+IMG = os.environ.get("GEMM_IMG", "1") != "0"
 L = hip.lib()
 
 
@@ -35,14 +38,15 @@ for M, K in shapes:
     aos = torch.from_numpy(mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))).cuda()
     w = torch.empty(hip.q4_bytes(M, K), dtype=torch.uint8, device="cuda")
     hip.check(L.vsim_op_q4_repack(aos.data_ptr(), w.data_ptr(), M, K, None), "repack")
-    img = torch.empty(M * K, dtype=torch.float16, device="cuda")
-    hip.check(L.vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    img = torch.empty(M * K if IMG else 8, dtype=torch.float16, device="cuda")
+    if IMG:
+        hip.check(L.vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
     x = torch.empty(N * K, dtype=torch.float16, device="cuda").normal_(0, 0.5)
     y = torch.empty(N * M, dtype=torch.float32, device="cuda")
     fq = lambda: hip.check(L.vsim_op_gemm_q4_256(w.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None, None,
                                                  0, 0, 0, 0, None, None), "q4")
     fi = lambda: hip.check(L.vsim_op_gemm_f16(img.data_ptr(), M, K, x.data_ptr(), N, None, y.data_ptr(), None), "img")
-    for name, f in (("q4 (model kernel)", fq), ("fp16 image", fi)):
+    for name, f in (("q4 (model kernel)", fq), ("fp16 image", fi))[:2 if IMG else 1]:
         ms = timeit(f)
         print(f"M={M} K={K} N={N} {name:18s}: {ms * 1e3:.1f} us  {2.0 * M * K * N / ms / 1e9:.0f} TFLOP/s", flush=True)
     del aos, w, img, x, y
