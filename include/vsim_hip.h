@@ -192,6 +192,11 @@ int vsim_op_attn_prefill(const float *Q, const float *kc, const float *vc, int d
  * d*(q-8) as fp16 -- what vsim_op_act_quant_f16 makes of vsim_op_attn_prefill's out. */
 int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
                              float scale, void *out16, void *stream);
+/* The long-prompt GEMM (vsim_op_gemm_q4_256, the model's N >= 256 path) splits the K range of
+ * grids with fewer 256 x 256 tiles than CUs between two workgroups (stream-K: every CU busy, the
+ * two partial sums added once; a different summation order than one pass, same per-element
+ * bound).  enable = 0 keeps one pass per tile.  Process-wide; returns the previous setting. */
+int vsim_gemm_set_streamk(int enable);
 /* device fp16 tables (exp, gelu) as built by ggml_init (ggml.c:1240-1251) */
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host);
 

@@ -476,6 +476,15 @@ def test_prefill_gemm_q4_in_lds_dequant_bit_identical(M, K, N):
     img = torch.empty(M * K, dtype=torch.float16, device=DEV)
     L = hip.lib()
     hip.check(L.vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    # one pass per tile (a stream-K split sums in another order: test_prefill_gemm_streamk_bound)
+    was = L.vsim_gemm_set_streamk(0)
+    try:
+        _q4_vs_image(L, M, K, N, rng, w, img)
+    finally:
+        L.vsim_gemm_set_streamk(was)
+
+
+def _q4_vs_image(L, M, K, N, rng, w, img):
     x = torch.from_numpy((rng.standard_normal((N, K)) * 0.5).astype(np.float16)).to(DEV)
     bd = dev((rng.standard_normal(M) * 0.1).astype(np.float32))
 
@@ -509,6 +518,49 @@ def test_prefill_gemm_q4_in_lds_dequant_bit_identical(M, K, N):
         both(lambda r: L.vsim_op_gemm_f16_join(ip, M, K, xp, N, bp, r.data_ptr(), A.data_ptr(), None),
              lambda r: L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, r.data_ptr(), None, None, 0, 0, 0, 1, A.data_ptr(),
                                              None), init=R)
+
+
+@pytest.mark.parametrize("M,K,N", [(6144, 6144, 2048), (6144, 4096, 1800), (6144, 24576, 2048)])
+def test_prefill_gemm_streamk_bound(M, K, N):
+    """Grids with fewer tiles than CUs (every 6144-row codegen-16B GEMM) split each tile's K range
+    between two workgroups and add the partial sums once.  Against one pass per tile: the same
+    products in another order, so per element |y_sk - y_1| <= 2 K 2^-24 sum_k |w_k x_k| (the
+    bound both orders obey); plain and residual-join epilogues, repeated runs bit-identical."""
+    rng = np.random.default_rng(M + K + N)
+    w = repack(mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05)), M, K)
+    img = torch.empty(M * K, dtype=torch.float16, device=DEV)
+    L = hip.lib()
+    hip.check(L.vsim_op_q4_expand_f16(w.data_ptr(), M, K, img.data_ptr(), None), "expand")
+    x = torch.from_numpy((rng.standard_normal((N, K)) * 0.5).astype(np.float16)).to(DEV)
+    bd = dev((rng.standard_normal(M) * 0.1).astype(np.float32))
+    res = dev((rng.standard_normal(N * M)).astype(np.float32))
+    wp, xp, bp = w.data_ptr(), x.data_ptr(), bd.data_ptr()
+
+    def plain(y):
+        return L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, y.data_ptr(), None, None, 0, 0, 0, 0, None, None)
+
+    def join(y):
+        return L.vsim_op_gemm_q4_256(wp, M, K, xp, N, bp, y.data_ptr(), None, None, 0, 0, 0, 1, None, None)  # y = res
+
+    absprod = (x.float().abs() @ img.view(M, K).float().abs().t()).reshape(-1)
+    tol = 2.0 * K * 2.0 ** -24 * absprod
+    was = L.vsim_gemm_set_streamk(1)
+    try:
+        for fn, init in ((plain, None), (join, res)):
+            outs = {}
+            for sk in (0, 1, 1):
+                L.vsim_gemm_set_streamk(sk)
+                y = torch.empty(N * M, device=DEV) if init is None else init.clone()
+                hip.check(fn(y), "gemm")
+                outs.setdefault(sk, []).append(y)
+            torch.cuda.synchronize()
+            a, b, b2 = outs[0][0], outs[1][0], outs[1][1]
+            assert torch.equal(b.view(torch.int32), b2.view(torch.int32)), "stream-K not deterministic"
+            err = (a - b).abs()
+            assert bool((err <= tol + 1e-30).all()), float((err / (tol + 1e-30)).max())
+            assert int((err > 0).sum()) > 0 or K <= 128  # (the split really ran)
+    finally:
+        L.vsim_gemm_set_streamk(was)
 
 
 @pytest.mark.parametrize("H,N,n_past", [(2, 200, 0), (3, 300, 37), (1, 64, 130)])

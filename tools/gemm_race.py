@@ -21,7 +21,8 @@ def main():
     L = hip.lib()
     g = torch.Generator(device="cuda").manual_seed(7)
     bad = 0
-    for M, K, N in [(6144, 6144, 2048), (24576, 1024, 2048), (1056, 128, 257), (512, 4096, 300)]:
+    for M, K, N in [(6144, 6144, 2048), (24576, 1024, 2048), (1056, 128, 257), (512, 4096, 300), (6144, 24576, 2048),
+                    (6144, 4096, 1800)]:
         aos = torch.from_numpy(mg.quantize_q4_0(np.random.default_rng(M + K).standard_normal(M * K).astype(
             np.float32) * np.float32(0.05))).cuda()
         wq = torch.empty(hip.q4_bytes(M, K), dtype=torch.uint8, device="cuda")

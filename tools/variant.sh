@@ -7,10 +7,12 @@ cd "$(dirname "$0")/../vsim_amd"
 name=$1; src=$2; flags=$3; alt=${4:-csrc/$2}
 mkdir -p _build/var
 objs=""
+extra=""
+case $(basename $src) in gemm_f16.hip|gemv_chain.hip) extra=-fno-slp-vectorize;; esac  # (the Makefile's per-file flags)
 for o in _build/*.o; do
   b=$(basename $o .o)
   if [ "$b" = "$(basename $src)" ]; then
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include $flags -c $alt -o _build/var/$name.o
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include $extra $flags -c $alt -o _build/var/$name.o
     objs="$objs _build/var/$name.o"
   else
     objs="$objs $o"

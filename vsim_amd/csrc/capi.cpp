@@ -153,6 +153,7 @@ int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, i
                                  out16);
 }
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host) { return tables_host(exp_f16_host, gelu_f16_host); }
+int vsim_gemm_set_streamk(int enable) { return gemm_set_streamk(enable); }
 
 }  // extern "C"
 

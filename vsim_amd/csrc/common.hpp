@@ -310,6 +310,7 @@ int launch_gemm_q4_256(const W4 &W, const void *x16, int n, const float *bias, f
                        void *q16 = nullptr, const G2Epi *epi = nullptr);
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
                         hipStream_t s, void *q16 = nullptr, const G2Epi *epi = nullptr);
+int gemm_set_streamk(int on);  // stream-K split of the register-dequant GEMM (default on); returns the old setting
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call); fresh: the new keys [n_past, n_past + N) are

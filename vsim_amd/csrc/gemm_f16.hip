@@ -17,6 +17,9 @@
 // a scale into 32 halves -- with the fp8 nibble conversion of the exact GEMV (an e4m3 byte
 // n in 0..15 is n * 2^-9).  The next step's units are loaded into registers before the
 // MFMAs of the current step, so their global latency hides behind the matrix work.
+#include <map>
+#include <mutex>
+
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
@@ -667,82 +670,99 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_f16_256(const _Float16 *
 constexpr int R_BM = 256;
 constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
 
-template <bool GQ, int EM>
+// Stream-K (sk.upw > 0, for grids of fewer tiles than CUs: the 192 tiles of every 6144-row
+// codegen-16B GEMM): the grid is one workgroup per CU and workgroup b takes the K-tile pairs
+// ("units") [b upw, (b + 1) upw) of the tiles laid end to end, so every CU does the same work.
+// A tile split between two workgroups: the one holding its start (the lower index) computes that
+// part first thing and publishes its accumulators (write-through sc1 stores in the register
+// layout, drained, then an sc1 flag holding this launch's epoch); the one holding its end
+// computes that part last, polls the flag (sc1), adds the partial with sc1 loads (one rounded
+// add per value: partial + own, the same in every run) and runs the epilogue.  Waits only on
+// lower-indexed workgroups, dispatched before it; the launcher checks no tile has 3 pieces.
+struct RSk {
+  int upw = 0;          // units (K-tile pairs) per workgroup; 0: one tile per workgroup
+  float *ws = nullptr;  // partials: [tile][wave][32 f32x4][64 lanes]
+  unsigned *flags = nullptr;
+  unsigned epoch = 0;
+};
+
+template <bool GQ, int EM, bool SK = false>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, int K, const _Float16 *__restrict__ B,
                                                              int N, const float *__restrict__ bias, float *__restrict__ Y,
                                                              const uint16_t *__restrict__ gelu_tab,
-                                                             _Float16 *__restrict__ Q16, const G2Epi epi) {
+                                                             _Float16 *__restrict__ Q16, const G2Epi epi, const RSk sk) {
   extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2;
   const int tm = (M + R_BM - 1) / R_BM, tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
-  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int m0 = (wg / tn) * R_BM, n0 = (wg % tn) * G2_BN;
   const int nk = K / G2_BK, nb = K / QK;
   const uint32_t lbase = lds_addr(g2lds);
-  auto stage = [&](int kt, int q) {  // B piece q of K-tile kt into buffer kt & 1 (clamped source tile)
-    const int kc = min(kt, nk - 1);
-    const int r = wave * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (r & 7);
-    const int grow = min(n0 + q * 64 + r, N - 1);
-    glds16<false>(B + (size_t)grow * K + (size_t)kc * G2_BK + 8 * c,
-                  lbase + (uint32_t)((((kt & 1) * 4 + q) * G2_PIECE + wave * 8 * G2_BK) * 2));
-  };
   const int fr = lane & 15, fk = lane >> 4;
-  const int qt = min(m0 / T32 + wave, (M + T32 - 1) / T32 - 1);  // (clamped: rows past M are not stored)
-  const uint8_t *qbase = WQ.qs + ((size_t)qt * nb * T32 + fr) * 16 + 4 * fk;
-  const float *dbase = WQ.d + (size_t)qt * nb * T32 + fr;
-  // raw fragment f = 2 i + kk of K-tile kt: word fk of block 2 kt + kk of row 16 i + fr, its scale
-  auto rload = [&](int kt, int f, uint32_t &w, float &d) {
-    const size_t o = (size_t)(2 * min(kt, nk - 1) + (f & 1)) * T32 + 16 * (f >> 1);
-    asm volatile("global_load_dword %0, %1, off" : "=v"(w) : "v"(qbase + o * 16) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(dbase + o) : "memory");
-  };
   f32x4 acc[2][16];
+  // K-tiles [kt0, kt0 + nkt) of the tile at (m0, n0) into acc (nkt even, >= 2)
+  auto run = [&](int m0, int n0, int kt0, int nkt) __attribute__((always_inline)) {
+    // (the K range's offset folded into the base pointers: the loop's addressing is the whole-K one)
+    const _Float16 *Bk = B + (size_t)kt0 * G2_BK;
+    auto stage = [&](int kt, int q) {  // B piece q of K-tile kt into buffer kt & 1 (clamped source tile)
+      const int kc = min(kt, nkt - 1);
+      const int r = wave * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      const int grow = min(n0 + q * 64 + r, N - 1);
+      glds16<false>(Bk + (size_t)grow * K + (size_t)kc * G2_BK + 8 * c,
+                    lbase + (uint32_t)((((kt & 1) * 4 + q) * G2_PIECE + wave * 8 * G2_BK) * 2));
+    };
+    const int qt = min(m0 / T32 + wave, (M + T32 - 1) / T32 - 1);  // (clamped: rows past M are not stored)
+    const uint8_t *qbase = WQ.qs + ((size_t)qt * nb * T32 + fr) * 16 + 4 * fk + (size_t)2 * kt0 * T32 * 16;
+    const float *dbase = WQ.d + (size_t)qt * nb * T32 + fr + (size_t)2 * kt0 * T32;
+    // raw fragment f = 2 i + kk of K-tile kt: word fk of block 2 kt + kk of row 16 i + fr, its scale
+    auto rload = [&](int kt, int f, uint32_t &w, float &d) {
+      const size_t o = (size_t)(2 * min(kt, nkt - 1) + (f & 1)) * T32 + 16 * (f >> 1);
+      asm volatile("global_load_dword %0, %1, off" : "=v"(w) : "v"(qbase + o * 16) : "memory");
+      asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(dbase + o) : "memory");
+    };
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  uint32_t rw[2][4];
-  float rd[2][4];
-  half8 a[2][4], bq[4][2];
-  auto rdB = [&](int buf, int q) {
-    const _Float16 *bp = g2lds + (buf * 4 + q) * G2_PIECE;
+      for (int j = 0; j < 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    uint32_t rw[2][4];
+    float rd[2][4];
+    half8 a[2][4], bq[4][2];
+    auto rdB = [&](int buf, int q) {
+      const _Float16 *bp = g2lds + (buf * 4 + q) * G2_PIECE;
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
+      for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int row = 16 * jj + fr, c = kk * 4 + fk;
-        bq[jj][kk] = *(const half8 *)(bp + row * G2_BK + 8 * (c ^ (row & 7)));
-      }
-  };
-  // prologue: raw tile 0 and fragments 0-1 of tile 1, then the ops of phases -6 and -5 of the
-  // loop's order; tile 0 dequantized; then phases -4 .. -1 (their raw loads reuse tile 0's set)
+        for (int kk = 0; kk < 2; ++kk) {
+          const int row = 16 * jj + fr, c = kk * 4 + fk;
+          bq[jj][kk] = *(const half8 *)(bp + row * G2_BK + 8 * (c ^ (row & 7)));
+        }
+    };
+    // prologue: raw tile 0 and fragments 0-1 of tile 1, then the ops of phases -6 and -5 of the
+    // loop's order; tile 0 dequantized; then phases -4 .. -1 (their raw loads reuse tile 0's set)
 #pragma unroll
-  for (int f = 0; f < 4; ++f) rload(0, f, rw[0][f], rd[0][f]);
-  rload(1, 0, rw[1][0], rd[1][0]);
-  rload(1, 1, rw[1][1], rd[1][1]);
-  stage(0, 0);
-  rload(1, 2, rw[1][2], rd[1][2]);
-  stage(0, 1);
-  rload(1, 3, rw[1][3], rd[1][3]);
-  asm volatile("s_waitcnt vmcnt(10)" : "+v"(rw[0][0]), "+v"(rw[0][1]), "+v"(rw[0][2]), "+v"(rw[0][3]), "+v"(rd[0][0]),
-               "+v"(rd[0][1]), "+v"(rd[0][2]), "+v"(rd[0][3])::"memory");
+    for (int f = 0; f < 4; ++f) rload(0, f, rw[0][f], rd[0][f]);
+    rload(1, 0, rw[1][0], rd[1][0]);
+    rload(1, 1, rw[1][1], rd[1][1]);
+    stage(0, 0);
+    rload(1, 2, rw[1][2], rd[1][2]);
+    stage(0, 1);
+    rload(1, 3, rw[1][3], rd[1][3]);
+    asm volatile("s_waitcnt vmcnt(10)" : "+v"(rw[0][0]), "+v"(rw[0][1]), "+v"(rw[0][2]), "+v"(rw[0][3]), "+v"(rd[0][0]),
+                 "+v"(rd[0][1]), "+v"(rd[0][2]), "+v"(rd[0][3])::"memory");
 #pragma unroll
-  for (int f = 0; f < 4; ++f) a[0][f] = deq_word_f16(rw[0][f], rd[0][f]);
-  stage(0, 2);
-  rload(2, 0, rw[0][0], rd[0][0]);
-  stage(0, 3);
-  rload(2, 1, rw[0][1], rd[0][1]);
-  stage(1, 0);
-  rload(2, 2, rw[0][2], rd[0][2]);
-  stage(1, 1);
-  rload(2, 3, rw[0][3], rd[0][3]);
-  asm volatile("s_waitcnt vmcnt(14)" : "+v"(rw[1][0])::"memory");  // B pieces 0, 1 of tile 0
-  __builtin_amdgcn_s_barrier();
-  if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
-  // one phase: P = t & 1 (the parity of K-tile t), p = 0..3
+    for (int f = 0; f < 4; ++f) a[0][f] = deq_word_f16(rw[0][f], rd[0][f]);
+    stage(0, 2);
+    rload(2, 0, rw[0][0], rd[0][0]);
+    stage(0, 3);
+    rload(2, 1, rw[0][1], rd[0][1]);
+    stage(1, 0);
+    rload(2, 2, rw[0][2], rd[0][2]);
+    stage(1, 1);
+    rload(2, 3, rw[0][3], rd[0][3]);
+    asm volatile("s_waitcnt vmcnt(14)" : "+v"(rw[1][0])::"memory");  // B pieces 0, 1 of tile 0
+    __builtin_amdgcn_s_barrier();
+    if (wr) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+    // one phase: P = t & 1 (the parity of K-tile t), p = 0..3
 #define R_PHASE(t, P, p)                                                                                       \
   {                                                                                                            \
     rdB(P, p);                                                                                                 \
@@ -766,31 +786,172 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
       asm volatile("s_waitcnt vmcnt(14)" : "+v"(rw[P][0]), "+v"(rd[P][0])::"memory");                          \
     __builtin_amdgcn_s_barrier();                                                                              \
   }
-  for (int t = 0; t < nk; t += 2) {
-    R_PHASE(t, 0, 0)
-    R_PHASE(t, 0, 1)
-    R_PHASE(t, 0, 2)
-    R_PHASE(t, 0, 3)
-    R_PHASE(t + 1, 1, 0)
-    R_PHASE(t + 1, 1, 1)
-    R_PHASE(t + 1, 1, 2)
-    R_PHASE(t + 1, 1, 3)
-  }
+    for (int t = 0; t < nkt; t += 2) {
+      R_PHASE(t, 0, 0)
+      R_PHASE(t, 0, 1)
+      R_PHASE(t, 0, 2)
+      R_PHASE(t, 0, 3)
+      R_PHASE(t + 1, 1, 0)
+      R_PHASE(t + 1, 1, 1)
+      R_PHASE(t + 1, 1, 2)
+      R_PHASE(t + 1, 1, 3)
+    }
 #undef R_PHASE
-  if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped loads past the end have landed
-  __syncthreads();
-  // the wave's 32 rows x 256 columns
-  g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 + 32 * wave, n0, M, N, bias, Y, gelu_tab, Q16, epi, g2lds, wave,
-                                              lane);
+    if (!wr) __builtin_amdgcn_s_barrier();  // (pairs with group 1's last barrier)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped loads past the end have landed
+    __syncthreads();
+  };
+  auto epilogue = [&](int m0, int n0) __attribute__((always_inline)) {  // the wave's 32 rows x 256 columns
+    g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 + 32 * wave, n0, M, N, bias, Y, gelu_tab, Q16, epi, g2lds, wave,
+                                                lane);
+  };
+  if constexpr (!SK) {
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int m0 = (wg / tn) * R_BM, n0 = (wg % tn) * G2_BN;
+    run(m0, n0, 0, nk);
+    epilogue(m0, n0);
+  } else {
+    // [u0, u1) meets at most two tiles (the launcher checks): the end of tA (from unit aA) and
+    // the start of tA + 1.  Straight-line code, no loop over pieces: values of the second piece
+    // must not be hoisted above the first's K loop (the counted waits allow no spill traffic).
+    const int nu = nk / 2;
+    const int u0 = (int)blockIdx.x * sk.upw, u1 = min(u0 + sk.upw, nwg * nu);
+    const int tA = u0 / nu, aA = u0 - tA * nu, eA = min(u1 - tA * nu, nu);
+    const int eB = max(u1 - (tA + 1) * nu, 0);  // units of tA + 1 from its start
+    // first: the piece that starts a tile and is finished by the next workgroup (published)
+    const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
+    if (pubA || pubB) {
+      const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
+      run((t / tn) * R_BM, (t % tn) * G2_BN, 0, 2 * e);
+      float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
+      // (4 stores per base address, offsets 0-3 KB)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; j += 4) {
+          asm volatile(
+              "global_store_dwordx4 %0, %1, off sc1\n\t"
+              "global_store_dwordx4 %0, %2, off offset:1024 sc1\n\t"
+              "global_store_dwordx4 %0, %3, off offset:2048 sc1\n\t"
+              "global_store_dwordx4 %0, %4, off offset:3072 sc1" ::"v"(wp),
+              "v"(acc[i][j]), "v"(acc[i][j + 1]), "v"(acc[i][j + 2]), "v"(acc[i][j + 3])
+              : "memory");
+          wp += 4 * 256;
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(sk.flags + t, sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pubA) return;  // (tA's start was the whole range)
+    }
+    // then the piece this workgroup finishes: tA from aA (after a published tA + 1 start), or
+    // tA + 1 whole / tA whole
+    const bool finA = !pubA;
+    const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
+    if (!finA && e < nu) return;
+    run((t / tn) * R_BM, (t % tn) * G2_BN, 2 * a, 2 * (e - a));
+    if (a > 0) {  // the earlier part's partial
+      if (tid == 0)
+        while (__hip_atomic_load(sk.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sk.epoch)
+          __builtin_amdgcn_s_sleep(2);
+      __syncthreads();
+      const float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {  // 4 registers' worth at a time (acc holds 128 VGPRs)
+        f32x4 pv[4];
+        asm volatile(
+            "global_load_dwordx4 %0, %4, off sc1\n\t"
+            "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+            "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
+            "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(pv[0]), "=&v"(pv[1]), "=&v"(pv[2]), "=&v"(pv[3])
+            : "v"(wp)
+            : "memory");
+        wp += 4 * 256;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[g >> 2][4 * (g & 3) + q] = pv[q] + acc[g >> 2][4 * (g & 3) + q];
+      }
+    }
+    epilogue((t / tn) * R_BM, (t % tn) * G2_BN);
+  }
+}
+
+// Stream-K workspace per stream (partials + flags), grown on demand; the epoch tells one
+// launch's flags from the last one's, so the flags are never cleared.
+struct SkWs {
+  float *ws = nullptr;
+  unsigned *flags = nullptr;
+  int tiles = 0;
+  unsigned epoch = 0;
+};
+#ifndef VSIM_STREAMK  // (A/B builds: 0 keeps one tile per workgroup)
+#define VSIM_STREAMK 1
+#endif
+constexpr int SK_CUS = 256;
+static int g_streamk = 1;  // vsim_gemm_set_streamk
+int gemm_set_streamk(int on) {
+  const int was = g_streamk;
+  g_streamk = on ? 1 : 0;
+  return was;
 }
 
 template <bool GQ, int EM>
-static void r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, const uint16_t *tab,
-                 void *q16, const G2Epi &epi, hipStream_t s) {
+static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, const uint16_t *tab,
+                void *q16, const G2Epi &epi, hipStream_t s) {
   const int nwg = ((M + R_BM - 1) / R_BM) * ((n + G2_BN - 1) / G2_BN);
-  hipLaunchKernelGGL((k_gemm_q4r<GQ, EM>), dim3(nwg), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K, (const _Float16 *)x16,
-                     n, bias, y, tab, (_Float16 *)q16, epi);
+  RSk sk;
+  int grid = nwg;
+  const int nu = K / G2_BK / 2;
+  if (VSIM_STREAMK && g_streamk && !GQ && nwg < SK_CUS && nwg * 4 >= SK_CUS * 3 && nu >= 2) {
+    const int upw = (nwg * nu + SK_CUS - 1) / SK_CUS;
+    // every tile in at most two pieces (a piece strictly inside a tile would need a third)
+    bool two = true;
+    for (int t = 0; t < nwg && two; ++t) {
+      const int b0 = t * nu / upw, b1 = ((t + 1) * nu - 1) / upw;
+      two = b1 - b0 <= 1;
+    }
+    if (two) {
+      static std::mutex mu;
+      static std::map<hipStream_t, SkWs> per_stream;
+      std::lock_guard<std::mutex> lock(mu);
+      SkWs &w = per_stream[s];
+      if (w.tiles < nwg) {
+        if (w.ws) {
+          VSIM_HIP(hipStreamSynchronize(s));
+          VSIM_HIP(hipFree(w.ws));
+          VSIM_HIP(hipFree(w.flags));
+        }
+        VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)nwg * 8 * 32 * 64 * 16));
+        VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)nwg * sizeof(unsigned)));
+        VSIM_HIP(hipMemset(w.flags, 0, (size_t)nwg * sizeof(unsigned)));
+        w.tiles = nwg;
+        w.epoch = 0;
+      }
+      if (++w.epoch == 0) ++w.epoch;  // (0 is the cleared flag)
+      sk.upw = upw;
+      sk.ws = w.ws;
+      sk.flags = w.flags;
+      sk.epoch = w.epoch;
+      grid = (nwg * nu + upw - 1) / upw;
+    }
+  }
+  if constexpr (!GQ) {
+    if (sk.upw) {
+      static bool attr = false;
+      if (!attr) {
+        VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_q4r<GQ, EM, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     r_lds_bytes()));
+        attr = true;
+      }
+      hipLaunchKernelGGL((k_gemm_q4r<GQ, EM, true>), dim3(grid), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K,
+                         (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16, epi, sk);
+      return VSIM_OK;
+    }
+  }
+  hipLaunchKernelGGL((k_gemm_q4r<GQ, EM>), dim3(grid), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K, (const _Float16 *)x16,
+                     n, bias, y, tab, (_Float16 *)q16, epi, sk);
+  return VSIM_OK;
 }
 
 static int r_launch(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, hipStream_t s,
@@ -804,11 +965,13 @@ static int r_launch(const W4 &WQ, int M, int K, const void *x16, int n, const fl
       VSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
     attr = true;
   }
-  if (q16) r_go<true, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
-  else if (epi.cs) r_go<false, 1>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
-  else if (epi.res) r_go<false, 2>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
-  else if (epi.h16) r_go<false, 3>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
-  else r_go<false, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  int rc;
+  if (q16) rc = r_go<true, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else if (epi.cs) rc = r_go<false, 1>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else if (epi.res) rc = r_go<false, 2>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else if (epi.h16) rc = r_go<false, 3>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  else rc = r_go<false, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
+  if (rc) return rc;
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
