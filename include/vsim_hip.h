@@ -197,6 +197,10 @@ int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, i
  * two partial sums added once; a different summation order than one pass, same per-element
  * bound).  enable = 0 keeps one pass per tile.  Process-wide; returns the previous setting. */
 int vsim_gemm_set_streamk(int enable);
+/* Fast-mode prompt LayerNorm (ggml_norm + affine, ggml.c:4246-4304, double sums in any order)
+ * straight to the next GEMM's fp16 operand: quantize_row_q4_0 per 32-value block, d*(q-8) as
+ * fp16 -- what vsim_op_act_quant_f16 makes of the normalized rows. */
+int vsim_op_norm_f16q(const float *x, int k, int rows, const float *w, const float *b, void *x16, void *stream);
 /* device fp16 tables (exp, gelu) as built by ggml_init (ggml.c:1240-1251) */
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host);
 

@@ -563,6 +563,49 @@ def test_prefill_gemm_streamk_bound(M, K, N):
         L.vsim_gemm_set_streamk(was)
 
 
+def _q4_f16_ref(y):
+    """quantize_row_q4_0 (ggml.c:209-251) per 32-block of the f32 rows y, the values d*(q-8)
+    rounded once to fp16 (the prompt GEMMs' operand)."""
+    b = y.reshape(-1, 32).astype(np.float32)
+    amax = np.abs(b).max(axis=1).astype(np.float32)
+    d = (amax / np.float32(7.0)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1.0) / d, np.float32(0.0)).astype(np.float32)
+    t = (b * idv[:, None]).astype(np.float32)
+    q = np.where(t >= 0, np.floor(t + 0.5), -np.floor(-t + 0.5))  # round half away from zero
+    return (d[:, None].astype(np.float64) * q).astype(np.float16).reshape(y.shape)
+
+
+@pytest.mark.parametrize("k,rows", [(6144, 300), (4096, 257), (1024, 64), (5120, 33), (2080, 20)])
+def test_prompt_norm_f16q(k, rows):
+    """The fast-mode prompt LayerNorm + affine straight to the fp16 GEMM operand (one wave per row
+    for k % 256 == 0, the workgroup kernel otherwise) against numpy: the norm in double with the
+    reference's float steps, then quantize_row_q4_0 per block.  The double sums run in another
+    order, so a value may move by one quantization step where a rounding lands on a boundary:
+    nearly all values bit-equal, none off by more than a step."""
+    rng = np.random.default_rng(k + rows)
+    x = (rng.standard_normal((rows, k)) * 2.0 + 0.3).astype(np.float32)
+    w = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(k)).astype(np.float32)
+    out = torch.empty(rows * k, dtype=torch.float16, device=DEV)
+    xg, wg, bg = dev(x), dev(w), dev(b)  # (held: a temporary's memory could be reused before the launch)
+    hip.check(hip.lib().vsim_op_norm_f16q(xg.data_ptr(), k, rows, wg.data_ptr(), bg.data_ptr(), out.data_ptr(), None),
+              "norm_f16q")
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(rows, k)
+    xd = x.astype(np.float64)
+    mean = xd.sum(axis=1, keepdims=True) / k
+    var = ((xd - mean) ** 2).sum(axis=1, keepdims=True) / k
+    scale = (1.0 / np.sqrt(var + np.float64(np.float32(1e-5)))).astype(np.float32)
+    y = ((xd - mean).astype(np.float32) * scale).astype(np.float32)
+    y = (w[None, :] * y).astype(np.float32) + b[None, :]
+    want = _q4_f16_ref(y.astype(np.float32))
+    step = (np.abs(y.reshape(-1, 32)).max(axis=1) / 7.0).repeat(32).reshape(rows, k)
+    diff = np.abs(got.astype(np.float64) - want.astype(np.float64))
+    assert float((diff > 0).mean()) < 1e-3
+    assert bool((diff <= step * 1.001 + 1e-6).all())
+
+
 @pytest.mark.parametrize("H,N,n_past", [(2, 200, 0), (3, 300, 37), (1, 64, 130)])
 def test_attn_prefill_quantized_output_bit_identical(H, N, n_past):
     """d = 256: the attention writing the out-projection's fp16 operand itself

@@ -154,6 +154,9 @@ int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, i
 }
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host) { return tables_host(exp_f16_host, gelu_f16_host); }
 int vsim_gemm_set_streamk(int enable) { return gemm_set_streamk(enable); }
+int vsim_op_norm_f16q(const float *x, int k, int rows, const float *w, const float *b, void *x16, void *stream) {
+  return launch_norm_f16q(x, x16, k, rows, w, b, (hipStream_t)stream);
+}
 
 }  // extern "C"
 
