@@ -914,9 +914,11 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
     }
     if (two) {
       static std::mutex mu;
-      static std::map<hipStream_t, SkWs> per_stream;
+      static std::map<std::pair<int, hipStream_t>, SkWs> per_stream;  // (device, stream): a null stream is per device
+      int dev = 0;
+      VSIM_HIP(hipGetDevice(&dev));
       std::lock_guard<std::mutex> lock(mu);
-      SkWs &w = per_stream[s];
+      SkWs &w = per_stream[{dev, s}];
       if (w.tiles < nwg) {
         if (w.ws) {
           VSIM_HIP(hipStreamSynchronize(s));
