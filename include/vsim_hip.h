@@ -197,6 +197,17 @@ int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, i
  * two partial sums added once; a different summation order than one pass, same per-element
  * bound).  enable = 0 keeps one pass per tile.  Process-wide; returns the previous setting. */
 int vsim_gemm_set_streamk(int enable);
+/* Two long-prompt GEMMs of one shape with the RoPE epilogue (the GPT-J prompt's Q and K
+ * projections, vsim.cpp:540-580: ggml_mul_mat (ggml.c:4891-5165) then ggml_rope mode 0) in one
+ * launch: y0 = RoPE(w0 x), y1 = RoPE(w1 x), M % 256 == 0, K % 128 == 0, positions p0 + n.  The
+ * tile grid covers both; a remainder beyond whole rounds of the CUs is split as above.  Same
+ * per-element bound as vsim_op_gemm_q4_256 with cs. */
+int vsim_op_gemm_q4_256_pair(const void *w0, const void *w1, int M, int K, const void *x16, int n, float *y0, float *y1,
+                             const double *cs, int d, int n_rot, int p0, void *stream);
+/* mode 0: the model runs its prompt Q and K projections as two launches; 1 (default): one
+ * paired launch, its remainder past whole rounds of the CUs split as above; 2: paired, whole
+ * tiles only.  Process-wide; returns the previous setting. */
+int vsim_gemm_set_qk_pair(int mode);
 /* Fast-mode prompt LayerNorm (ggml_norm + affine, ggml.c:4246-4304, double sums in any order)
  * straight to the next GEMM's fp16 operand: quantize_row_q4_0 per 32-value block, d*(q-8) as
  * fp16 -- what vsim_op_act_quant_f16 makes of the normalized rows. */

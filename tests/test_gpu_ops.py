@@ -563,6 +563,74 @@ def test_prefill_gemm_streamk_bound(M, K, N):
         L.vsim_gemm_set_streamk(was)
 
 
+@pytest.mark.parametrize("M,K,N,p0", [(512, 256, 300, 0), (4096, 4096, 2048, 5), (6144, 6144, 2048, 3)])
+def test_prefill_gemm_qk_pair(M, K, N, p0):
+    """A long GPT-J prompt's Q and K projections as one launch (vsim_op_gemm_q4_256_pair, both
+    RoPE epilogues) against two single launches of one pass per tile.  Without the split the
+    pair is bit-identical (every shape).  With it, the tiles past whole rounds of the CUs (the
+    codegen-16B pair: 384 tiles, the last 128 halved over 256 workgroups, all in the second
+    weight) add two partial sums: per element within the split bound 2 K 2^-24 sum_k |w_k x_k|
+    of the element and of its RoPE partner, plus one ulp of the rotation; the first weight's
+    tiles stay bit-identical; repeated runs are bit-identical."""
+    rng = np.random.default_rng(M + K + N + p0)
+    ws = [repack(mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.05)), M, K)
+          for _ in range(2)]
+    x = torch.from_numpy((rng.standard_normal((N, K)) * 0.5).astype(np.float16)).to(DEV)
+    d, n_rot = 256, 64
+    half = n_rot // 2
+    theta = np.arange(p0 + N, dtype=np.float64)[:, None] * 10000.0 ** (-2.0 * np.arange(half) / n_rot)[None, :]
+    cs = dev(np.ascontiguousarray(np.stack([np.cos(theta), np.sin(theta)], axis=-1)))
+    L = hip.lib()
+    xp, cp = x.data_ptr(), cs.data_ptr()
+
+    def single(w):
+        y = torch.empty(N * M, device=DEV)
+        hip.check(L.vsim_op_gemm_q4_256(w.data_ptr(), M, K, xp, N, None, y.data_ptr(), None, cp, d, n_rot, p0, 0,
+                                        None, None), "single")
+        return y
+
+    def pair():
+        y0, y1 = torch.empty(N * M, device=DEV), torch.empty(N * M, device=DEV)
+        hip.check(L.vsim_op_gemm_q4_256_pair(ws[0].data_ptr(), ws[1].data_ptr(), M, K, xp, N, y0.data_ptr(),
+                                             y1.data_ptr(), cp, d, n_rot, p0, None), "pair")
+        return y0, y1
+
+    was = L.vsim_gemm_set_streamk(0)
+    try:
+        ref = [single(w) for w in ws]
+        p0_, p1_ = pair()
+        torch.cuda.synchronize()
+        assert torch.equal(p0_.view(torch.int32), ref[0].view(torch.int32))
+        assert torch.equal(p1_.view(torch.int32), ref[1].view(torch.int32))
+        L.vsim_gemm_set_streamk(1)
+        mode = L.vsim_gemm_set_qk_pair(2)  # (paired, whole tiles only: bit-identical with the split allowed)
+        try:
+            c0, c1 = pair()
+        finally:
+            L.vsim_gemm_set_qk_pair(mode)
+        (a0, a1), (b0, b1) = pair(), pair()
+        torch.cuda.synchronize()
+        assert torch.equal(c0.view(torch.int32), ref[0].view(torch.int32))
+        assert torch.equal(c1.view(torch.int32), ref[1].view(torch.int32))
+    finally:
+        L.vsim_gemm_set_streamk(was)
+    assert torch.equal(a0.view(torch.int32), b0.view(torch.int32)) and torch.equal(a1.view(torch.int32),
+                                                                                      b1.view(torch.int32))
+    assert torch.equal(a0.view(torch.int32), ref[0].view(torch.int32))
+    img = torch.empty(M * K, dtype=torch.float16, device=DEV)
+    hip.check(L.vsim_op_q4_expand_f16(ws[1].data_ptr(), M, K, img.data_ptr(), None), "expand")
+    torch.cuda.synchronize()
+    absprod = (x.float().abs() @ img.view(M, K).float().abs().t())  # [N][M]
+    tol = 2.0 * K * 2.0 ** -24 * absprod
+    col = torch.arange(M, device=DEV)
+    partner = torch.where(col % d < n_rot, col ^ 1, col)  # GPT-J RoPE rotates adjacent pairs
+    tol = (tol + tol[:, partner]).reshape(-1) + 2.0 ** -23 * ref[1].abs()
+    err = (a1 - ref[1]).abs()
+    assert bool((err <= tol + 1e-30).all()), float((err / (tol + 1e-30)).max())
+    if M * 2 // 256 * ((N + 255) // 256) > 256:
+        assert int((err > 0).sum()) > 0  # (the split really ran)
+
+
 def _q4_f16_ref(y):
     """quantize_row_q4_0 (ggml.c:209-251) per 32-block of the f32 rows y, the values d*(q-8)
     rounded once to fp16 (the prompt GEMMs' operand)."""

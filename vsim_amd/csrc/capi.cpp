@@ -154,6 +154,20 @@ int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, i
 }
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host) { return tables_host(exp_f16_host, gelu_f16_host); }
 int vsim_gemm_set_streamk(int enable) { return gemm_set_streamk(enable); }
+int vsim_gemm_set_qk_pair(int mode) { return gemm_set_qk_pair(mode); }
+int vsim_op_gemm_q4_256_pair(const void *w0, const void *w1, int M, int K, const void *x16, int n, float *y0, float *y1,
+                             const double *cs, int d, int n_rot, int p0, void *stream) {
+  if (!w0 || !w1 || !x16 || !y0 || !y1 || !cs || M <= 0 || K <= 0 || K % QK || p0 < 0 || n <= 0) {
+    set_error("gemm_q4_256_pair: bad argument");
+    return VSIM_EINVAL;
+  }
+  G2Epi e;
+  e.cs = (const double2 *)cs;
+  e.d = d;
+  e.n_rot = n_rot;
+  e.p0 = p0;
+  return launch_gemm_q4_256_pair(w4_view(w0, M, K), w4_view(w1, M, K), x16, n, y0, y1, e, e, (hipStream_t)stream);
+}
 int vsim_op_norm_f16q(const float *x, int k, int rows, const float *w, const float *b, void *x16, void *stream) {
   return launch_norm_f16q(x, x16, k, rows, w, b, (hipStream_t)stream);
 }

@@ -310,6 +310,12 @@ int launch_gemm_q4_256(const W4 &W, const void *x16, int n, const float *bias, f
                        void *q16 = nullptr, const G2Epi *epi = nullptr);
 int launch_gemm_f16_256(const void *A16, int M, int K, const void *x16, int n, const float *bias, float *y,
                         hipStream_t s, void *q16 = nullptr, const G2Epi *epi = nullptr);
+// the Q and K projections of a long GPT-J prompt (same M x K, RoPE epilogues) in one launch;
+// gemm_pair_enabled: the model takes it for this shape (else two launch_gemm_q4_256 calls)
+int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, float *y0, float *y1, const G2Epi &e0,
+                            const G2Epi &e1, hipStream_t s);
+bool gemm_pair_enabled(int M, int K);
+int gemm_set_qk_pair(int mode);  // vsim_gemm_set_qk_pair (0 off, 1 default, 2 no split); returns the old setting
 int gemm_set_streamk(int on);  // stream-K split of the register-dequant GEMM (default on); returns the old setting
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or

@@ -679,28 +679,45 @@ constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
 // computes that part last, polls the flag (sc1), adds the partial with sc1 loads (one rounded
 // add per value: partial + own, the same in every run) and runs the epilogue.  Waits only on
 // lower-indexed workgroups, dispatched before it; the launcher checks no tile has 3 pieces.
+// Hybrid split (PAIR launches, wg0 > 0): workgroups [0, wg0) take the whole tiles [0, wg0) (a
+// full round of the CUs), the rest run the split above over the tiles from t0 = wg0 on.
 struct RSk {
   int upw = 0;          // units (K-tile pairs) per workgroup; 0: one tile per workgroup
-  float *ws = nullptr;  // partials: [tile][wave][32 f32x4][64 lanes]
+  float *ws = nullptr;  // partials: [tile - t0][wave][32 f32x4][64 lanes]
   unsigned *flags = nullptr;
   unsigned epoch = 0;
+  int wg0 = 0, t0 = 0;
 };
 
-template <bool GQ, int EM, bool SK = false>
+// PAIR: two GEMMs of the same shape (M rows each: the Q and K projections of a long GPT-J
+// prompt, both with the RoPE epilogue) in one launch.  The tile grid covers 2M rows; tiles of
+// rows >= M are the second GEMM's (pr: its weight, output and epilogue).  One launch of 2x the
+// tiles fills the CUs where each alone leaves some idle or needs the split.
+struct RPair {
+  W4 w{};
+  float *y = nullptr;
+  G2Epi epi{};
+};
+
+template <bool GQ, int EM, bool SK = false, bool PAIR = false>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, int K, const _Float16 *__restrict__ B,
                                                              int N, const float *__restrict__ bias, float *__restrict__ Y,
                                                              const uint16_t *__restrict__ gelu_tab,
-                                                             _Float16 *__restrict__ Q16, const G2Epi epi, const RSk sk) {
+                                                             _Float16 *__restrict__ Q16, const G2Epi epi, const RSk sk,
+                                                             const RPair pr) {
   extern __shared__ __attribute__((aligned(16))) _Float16 g2lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2;
-  const int tm = (M + R_BM - 1) / R_BM, tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
+  const int tm = (PAIR ? 2 : 1) * ((M + R_BM - 1) / R_BM), tn = (N + G2_BN - 1) / G2_BN, nwg = tm * tn;
   const int nk = K / G2_BK, nb = K / QK;
   const uint32_t lbase = lds_addr(g2lds);
   const int fr = lane & 15, fk = lane >> 4;
   f32x4 acc[2][16];
   // K-tiles [kt0, kt0 + nkt) of the tile at (m0, n0) into acc (nkt even, >= 2)
   auto run = [&](int m0, int n0, int kt0, int nkt) __attribute__((always_inline)) {
+    const bool j2 = PAIR && m0 >= M;
+    const W4 WJ = j2 ? pr.w : WQ;
+    if (j2) m0 -= M;
     // (the K range's offset folded into the base pointers: the loop's addressing is the whole-K one)
     const _Float16 *Bk = B + (size_t)kt0 * G2_BK;
     auto stage = [&](int kt, int q) {  // B piece q of K-tile kt into buffer kt & 1 (clamped source tile)
@@ -712,8 +729,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
                     lbase + (uint32_t)((((kt & 1) * 4 + q) * G2_PIECE + wave * 8 * G2_BK) * 2));
     };
     const int qt = min(m0 / T32 + wave, (M + T32 - 1) / T32 - 1);  // (clamped: rows past M are not stored)
-    const uint8_t *qbase = WQ.qs + ((size_t)qt * nb * T32 + fr) * 16 + 4 * fk + (size_t)2 * kt0 * T32 * 16;
-    const float *dbase = WQ.d + (size_t)qt * nb * T32 + fr + (size_t)2 * kt0 * T32;
+    const uint8_t *qbase = WJ.qs + ((size_t)qt * nb * T32 + fr) * 16 + 4 * fk + (size_t)2 * kt0 * T32 * 16;
+    const float *dbase = WJ.d + (size_t)qt * nb * T32 + fr + (size_t)2 * kt0 * T32;
     // raw fragment f = 2 i + kk of K-tile kt: word fk of block 2 kt + kk of row 16 i + fr, its scale
     auto rload = [&](int kt, int f, uint32_t &w, float &d) {
       const size_t o = (size_t)(2 * min(kt, nkt - 1) + (f & 1)) * T32 + 16 * (f >> 1);
@@ -802,28 +819,42 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     __syncthreads();
   };
   auto epilogue = [&](int m0, int n0) __attribute__((always_inline)) {  // the wave's 32 rows x 256 columns
-    g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 + 32 * wave, n0, M, N, bias, Y, gelu_tab, Q16, epi, g2lds, wave,
-                                                lane);
+    if (PAIR && m0 >= M) {
+      g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 - M + 32 * wave, n0, M, N, bias, pr.y, gelu_tab, Q16, pr.epi,
+                                                  g2lds, wave, lane);
+    } else {
+      g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 + 32 * wave, n0, M, N, bias, Y, gelu_tab, Q16, epi, g2lds,
+                                                  wave, lane);
+    }
   };
-  if constexpr (!SK) {
-    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  // one whole tile per workgroup, the first `count` tiles, XCD-remapped
+  auto whole = [&](int count) __attribute__((always_inline)) {
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = count >> 3, r8 = count & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int m0 = (wg / tn) * R_BM, n0 = (wg % tn) * G2_BN;
     run(m0, n0, 0, nk);
     epilogue(m0, n0);
+  };
+  if constexpr (!SK) {
+    whole(nwg);
   } else {
+    if (PAIR && (int)blockIdx.x < sk.wg0) {
+      whole(sk.wg0);
+      return;
+    }
     // [u0, u1) meets at most two tiles (the launcher checks): the end of tA (from unit aA) and
     // the start of tA + 1.  Straight-line code, no loop over pieces: values of the second piece
     // must not be hoisted above the first's K loop (the counted waits allow no spill traffic).
     const int nu = nk / 2;
-    const int u0 = (int)blockIdx.x * sk.upw, u1 = min(u0 + sk.upw, nwg * nu);
+    const int t0 = PAIR ? sk.t0 : 0;  // (tile indices below count from t0)
+    const int u0 = ((int)blockIdx.x - (PAIR ? sk.wg0 : 0)) * sk.upw, u1 = min(u0 + sk.upw, (nwg - t0) * nu);
     const int tA = u0 / nu, aA = u0 - tA * nu, eA = min(u1 - tA * nu, nu);
     const int eB = max(u1 - (tA + 1) * nu, 0);  // units of tA + 1 from its start
     // first: the piece that starts a tile and is finished by the next workgroup (published)
     const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
     if (pubA || pubB) {
       const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
-      run((t / tn) * R_BM, (t % tn) * G2_BN, 0, 2 * e);
+      run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 0, 2 * e);
       float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
       // (4 stores per base address, offsets 0-3 KB)
 #pragma unroll
@@ -849,7 +880,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     const bool finA = !pubA;
     const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
     if (!finA && e < nu) return;
-    run((t / tn) * R_BM, (t % tn) * G2_BN, 2 * a, 2 * (e - a));
+    run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 2 * a, 2 * (e - a));
     if (a > 0) {  // the earlier part's partial
       if (tid == 0)
         while (__hip_atomic_load(sk.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sk.epoch)
@@ -873,7 +904,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
         for (int q = 0; q < 4; ++q) acc[g >> 2][4 * (g & 3) + q] = pv[q] + acc[g >> 2][4 * (g & 3) + q];
       }
     }
-    epilogue((t / tn) * R_BM, (t % tn) * G2_BN);
+    epilogue(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN);
   }
 }
 
@@ -896,6 +927,42 @@ int gemm_set_streamk(int on) {
   return was;
 }
 
+// the stream's split workspace for `tiles` split tiles (partials, flags, this launch's epoch)
+static int sk_workspace(int tiles, hipStream_t s, RSk &sk) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWs> per_stream;  // (device, stream): a null stream is per device
+  int dev = 0;
+  VSIM_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  SkWs &w = per_stream[{dev, s}];
+  if (w.tiles < tiles) {
+    if (w.ws) {
+      VSIM_HIP(hipStreamSynchronize(s));
+      VSIM_HIP(hipFree(w.ws));
+      VSIM_HIP(hipFree(w.flags));
+    }
+    VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 8 * 32 * 64 * 16));
+    VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)tiles * sizeof(unsigned)));
+    VSIM_HIP(hipMemset(w.flags, 0, (size_t)tiles * sizeof(unsigned)));
+    w.tiles = tiles;
+    w.epoch = 0;
+  }
+  if (++w.epoch == 0) ++w.epoch;  // (0 is the cleared flag)
+  sk.ws = w.ws;
+  sk.flags = w.flags;
+  sk.epoch = w.epoch;
+  return VSIM_OK;
+}
+
+// every split tile in at most two pieces (a piece strictly inside a tile would need a third)
+static bool sk_two_pieces(int tiles, int nu, int upw) {
+  for (int t = 0; t < tiles; ++t) {
+    const int b0 = t * nu / upw, b1 = ((t + 1) * nu - 1) / upw;
+    if (b1 - b0 > 1) return false;
+  }
+  return true;
+}
+
 template <bool GQ, int EM>
 static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, const uint16_t *tab,
                 void *q16, const G2Epi &epi, hipStream_t s) {
@@ -906,36 +973,9 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
   // (not for the V^T-copy epilogue: 167.0 vs 160.9 us per codegen-16B V GEMM with the split)
   if (VSIM_STREAMK && g_streamk && !GQ && EM != 3 && nwg < SK_CUS && nwg * 4 >= SK_CUS * 3 && nu >= 2) {
     const int upw = (nwg * nu + SK_CUS - 1) / SK_CUS;
-    // every tile in at most two pieces (a piece strictly inside a tile would need a third)
-    bool two = true;
-    for (int t = 0; t < nwg && two; ++t) {
-      const int b0 = t * nu / upw, b1 = ((t + 1) * nu - 1) / upw;
-      two = b1 - b0 <= 1;
-    }
-    if (two) {
-      static std::mutex mu;
-      static std::map<std::pair<int, hipStream_t>, SkWs> per_stream;  // (device, stream): a null stream is per device
-      int dev = 0;
-      VSIM_HIP(hipGetDevice(&dev));
-      std::lock_guard<std::mutex> lock(mu);
-      SkWs &w = per_stream[{dev, s}];
-      if (w.tiles < nwg) {
-        if (w.ws) {
-          VSIM_HIP(hipStreamSynchronize(s));
-          VSIM_HIP(hipFree(w.ws));
-          VSIM_HIP(hipFree(w.flags));
-        }
-        VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)nwg * 8 * 32 * 64 * 16));
-        VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)nwg * sizeof(unsigned)));
-        VSIM_HIP(hipMemset(w.flags, 0, (size_t)nwg * sizeof(unsigned)));
-        w.tiles = nwg;
-        w.epoch = 0;
-      }
-      if (++w.epoch == 0) ++w.epoch;  // (0 is the cleared flag)
+    if (sk_two_pieces(nwg, nu, upw)) {
+      if (int rc = sk_workspace(nwg, s, sk)) return rc;
       sk.upw = upw;
-      sk.ws = w.ws;
-      sk.flags = w.flags;
-      sk.epoch = w.epoch;
       grid = (nwg * nu + upw - 1) / upw;
     }
   }
@@ -948,12 +988,12 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
         attr = true;
       }
       hipLaunchKernelGGL((k_gemm_q4r<GQ, EM, true>), dim3(grid), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K,
-                         (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16, epi, sk);
+                         (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16, epi, sk, RPair{});
       return VSIM_OK;
     }
   }
   hipLaunchKernelGGL((k_gemm_q4r<GQ, EM>), dim3(grid), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K, (const _Float16 *)x16,
-                     n, bias, y, tab, (_Float16 *)q16, epi, sk);
+                     n, bias, y, tab, (_Float16 *)q16, epi, sk, RPair{});
   return VSIM_OK;
 }
 
@@ -982,6 +1022,65 @@ static int r_launch(const W4 &WQ, int M, int K, const void *x16, int n, const fl
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s) {
   const size_t n = (size_t)W.rows * (W.k / QK);
   hipLaunchKernelGGL(k_w4_expand_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, (half8 *)out);
+  VSIM_HIP(hipGetLastError());
+  return VSIM_OK;
+}
+
+// The Q and K projections of a long GPT-J prompt in one launch (RPair): two W4 weights of the
+// same M x K, both with the RoPE epilogue, no bias.  2 x 192 tiles for codegen-16B (E = 6144,
+// N = 2048): one full round of 256 whole tiles, then the other 128 split in halves over 256
+// workgroups (hybrid split); 2 x 128 for GPT-J-6B: exactly one round.
+static bool r_use(int K);
+static int g_qk_pair = 1;  // vsim_gemm_set_qk_pair: 0 off, 1 with the hybrid split, 2 whole tiles only
+int gemm_set_qk_pair(int mode) {
+  const int was = g_qk_pair;
+  g_qk_pair = mode < 0 || mode > 2 ? 1 : mode;
+  return was;
+}
+
+bool gemm_pair_enabled(int M, int K) { return g_qk_pair && M % R_BM == 0 && r_use(K); }
+
+int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, float *y0, float *y1, const G2Epi &e0,
+                            const G2Epi &e1, hipStream_t s) {
+  const int M = W0.rows, K = W0.k;
+  if (W1.rows != M || W1.k != K || M % R_BM || !r_use(K) || n <= 0 || !e0.cs || !e1.cs || e0.res || e1.res ||
+      (e0.h16 && e0.h16_t) || (e1.h16 && e1.h16_t) || e0.d <= 0 || e0.d % 2 || e0.n_rot % 2 || e0.n_rot > e0.d ||
+      e1.d != e0.d || e1.n_rot != e0.n_rot) {
+    set_error("gemm pair: two M x K weights (M % 256 == 0, K % 128 == 0) with RoPE epilogues of one head shape");
+    return VSIM_EINVAL;
+  }
+  static bool attr = false;
+  if (!attr) {
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_q4r<false, 1, false, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
+    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_q4r<false, 1, true, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
+    attr = true;
+  }
+  RPair pr;
+  pr.w = W1;
+  pr.y = y1;
+  pr.epi = e1;
+  const int nwg = 2 * (M / R_BM) * ((n + G2_BN - 1) / G2_BN), nu = K / G2_BK / 2;
+  RSk sk;
+  // hybrid split: the whole rounds as whole tiles, the remainder split over one round of CUs
+  const int wg0 = nwg / SK_CUS * SK_CUS, rest = nwg - wg0;
+  if (VSIM_STREAMK && g_streamk && g_qk_pair == 1 && wg0 > 0 && rest > 0 && nu >= 2) {
+    const int upw = (rest * nu + SK_CUS - 1) / SK_CUS;
+    if (upw < nu && sk_two_pieces(rest, nu, upw)) {
+      if (int rc = sk_workspace(rest, s, sk)) return rc;
+      sk.upw = upw;
+      sk.wg0 = wg0;
+      sk.t0 = wg0;
+      const int grid = wg0 + (rest * nu + upw - 1) / upw;
+      hipLaunchKernelGGL((k_gemm_q4r<false, 1, true, true>), dim3(grid), dim3(G2_THREADS), r_lds_bytes(), s, W0, M, K,
+                         (const _Float16 *)x16, n, nullptr, y0, nullptr, nullptr, e0, sk, pr);
+      VSIM_HIP(hipGetLastError());
+      return VSIM_OK;
+    }
+  }
+  hipLaunchKernelGGL((k_gemm_q4r<false, 1, false, true>), dim3(nwg), dim3(G2_THREADS), r_lds_bytes(), s, W0, M, K,
+                     (const _Float16 *)x16, n, nullptr, y0, nullptr, nullptr, e0, sk, pr);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

@@ -628,11 +628,19 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
     ev.h16_ld = attn_prefill_ldt(n_past + N);
     ev.p0 = n_past;
   }
-  // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547)
-  RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a, nullptr, nullptr,
-        nullptr, rope_epi ? &er : nullptr));
-  RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, kout, nk, X.a, nullptr, nullptr,
-        nullptr, rope_epi ? &ek : nullptr));
+  // Q, K, V (+ bias for GPT-NeoX, vsim.cpp:540-547); a long GPT-J prompt's Q and K (both RoPE
+  // epilogues, no bias) as one launch of both tile grids
+  if (rope_epi && gemm_pair_enabled(E, E)) {
+    const long ev = prof_begin(m);
+    RC(launch_gemm_q4_256_pair(w4_view(L.wq, E, E), w4_view(L.wk, E, E), X.a, N, m->Qb, kout, er, ek, s));
+    prof_end(m, ev, "k_gemm_f16_256 (prompt)", 2.0 * E * E / QK * QBYTES);
+    ++nk;
+  } else {
+    RC(mm(m, L.wq, E, E, m->cur1, N, m->xq1, m->xd1, true, gptj ? nullptr : L.bq, m->Qb, nk, X.a, nullptr, nullptr,
+          nullptr, rope_epi ? &er : nullptr));
+    RC(mm(m, L.wk, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bk, kout, nk, X.a, nullptr, nullptr,
+          nullptr, rope_epi ? &ek : nullptr));
+  }
   RC(mm(m, L.wv, E, E, m->cur1, N, m->xq1, m->xd1, false, gptj ? nullptr : L.bv, vout, nk, X.a, nullptr, nullptr,
         nullptr, kv16_epi ? &ev : nullptr));
   // KV write + RoPE (vsim.cpp:553-580)
