@@ -520,9 +520,11 @@ def _q4_vs_image(L, M, K, N, rng, w, img):
                                              None), init=R)
 
 
-@pytest.mark.parametrize("M,K,N", [(6144, 6144, 2048), (6144, 4096, 1800), (6144, 24576, 2048)])
+@pytest.mark.parametrize("M,K,N", [(6144, 6144, 2048), (6144, 4096, 1800), (6144, 24576, 2048), (4096, 4096, 2048),
+                                   (4096, 16384, 2048)])
 def test_prefill_gemm_streamk_bound(M, K, N):
-    """Grids with fewer tiles than CUs (every 6144-row codegen-16B GEMM) split each tile's K range
+    """Grids of at least half and fewer than all the CUs (every 6144-row codegen-16B GEMM, GPT-J-6B's
+    128 tiles at N = 2048) split each tile's K range
     between two workgroups and add the partial sums once.  Against one pass per tile: the same
     products in another order, so per element |y_sk - y_1| <= 2 K 2^-24 sum_k |w_k x_k| (the
     bound both orders obey); plain and residual-join epilogues, repeated runs bit-identical."""

@@ -30,7 +30,10 @@ for cfg in sys.argv[1:] or ["codegen-16B", "gpt-j-6B"]:
     logits = {}
     for r in range(len(modes) * (REPS + 1)):
         on = modes[r % len(modes)]
-        L.vsim_gemm_set_qk_pair(on)
+        if os.environ.get("AB_KNOB") == "streamk":  # (the same A/B over vsim_gemm_set_streamk modes)
+            L.vsim_gemm_set_streamk(on)
+        else:
+            L.vsim_gemm_set_qk_pair(on)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         lg = model.eval(0, ids)
@@ -39,7 +42,11 @@ for cfg in sys.argv[1:] or ["codegen-16B", "gpt-j-6B"]:
             times[on].append((time.perf_counter() - t0) * 1e3)
         logits.setdefault(on, lg)
     L.vsim_gemm_set_qk_pair(1)
-    out = {"config": cfg, "N": N, "modes": "0 separate launches, 1 pair + hybrid split, 2 pair, whole tiles"}
+    L.vsim_gemm_set_streamk(1)
+    knob = os.environ.get("AB_KNOB", "qk_pair")
+    out = {"config": cfg, "N": N, "knob": knob,
+           "modes": "stream-K off / on" if knob == "streamk" else
+                    "0 separate launches, 1 pair + hybrid split, 2 pair, whole tiles"}
     for m in modes:
         out[f"mode{m}_ms"] = [round(t, 2) for t in times[m]]
         out[f"mode{m}_median"] = round(sorted(times[m])[len(times[m]) // 2], 2)
