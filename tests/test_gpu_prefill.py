@@ -126,3 +126,28 @@ def test_codegen_width_prefill_n2048():
     print(msg)
     assert not np.isnan(lf).any()
     assert cos >= FAST_COS_MIN, msg
+
+
+GPTJ6B = dict(n_vocab=50400, n_embd=4096, n_head=16, n_layer=2, n_rot=64, use_parallel_residual=1)
+
+
+def test_gptj_width_prefill_n2048():
+    """GPT-J-6B width at N = 2048, fast path against exact mode on the same weights and tokens:
+    the paired Q/K launch (2 x 128 tiles, one round), the half-grid split of the 128-tile V
+    (transposed-copy epilogue), out-projection and fc_out GEMMs, end to end through two layers."""
+    N = 2048
+    dm = hip.Model.create(hip.ARCH_GPTJ, GPTJ6B, n_ctx=N + 8)
+    dm.randomize(seed=29, std=0.02)
+    ids = [(7919 * i + 11) % GPTJ6B["n_vocab"] for i in range(N)]
+    dm.set_mode(hip.MODE_EXACT)
+    le = dm.eval(0, ids)
+    dm.set_mode(hip.MODE_FAST)
+    lf = dm.eval(0, ids)
+    lf2 = dm.eval(0, ids)
+    cos, maxrel, same, _ = stats(lf, le)
+    msg = f"GPT-J-6B width, N=2048: cos {cos:.5f}, max-rel {maxrel:.3g}, top-1 {'same' if same else 'differs'}"
+    print(msg)
+    assert not np.isnan(lf).any()
+    assert np.array_equal(bits(lf), bits(lf2)), "fast prompt not deterministic"
+    assert cos >= FAST_COS_MIN, msg
+    dm.close()

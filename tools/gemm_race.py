@@ -21,8 +21,11 @@ def main():
     L = hip.lib()
     g = torch.Generator(device="cuda").manual_seed(7)
     bad = 0
-    for M, K, N in [(6144, 6144, 2048), (24576, 1024, 2048), (1056, 128, 257), (512, 4096, 300), (6144, 24576, 2048),
-                    (6144, 4096, 1800)]:
+    shapes = [(6144, 6144, 2048), (24576, 1024, 2048), (1056, 128, 257), (512, 4096, 300), (6144, 24576, 2048),
+              (6144, 4096, 1800), (4096, 4096, 2048), (4096, 16384, 2048)]
+    if os.environ.get("RACE_SHAPES"):  # "MxKxN,..."
+        shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["RACE_SHAPES"].split(",")]
+    for M, K, N in shapes:
         aos = torch.from_numpy(mg.quantize_q4_0(np.random.default_rng(M + K).standard_normal(M * K).astype(
             np.float32) * np.float32(0.05))).cuda()
         wq = torch.empty(hip.q4_bytes(M, K), dtype=torch.uint8, device="cuda")
@@ -32,6 +35,7 @@ def main():
         x = (torch.randn(N * K, device="cuda", generator=g) * 0.5).half()
         b = torch.randn(M, device="cuda", generator=g) * 0.1
         y = torch.empty(N * M, device="cuda")
+        y2 = torch.empty(N * M, device="cuda")
         q = torch.empty(N * M, dtype=torch.float16, device="cuda")
         half = 32
         pos = torch.arange(N + 3, dtype=torch.float64, device="cuda")[:, None]
@@ -52,6 +56,13 @@ def main():
             "q4_gelu": lambda: L.vsim_op_gemm_q4_256(wq.data_ptr(), M, K, x.data_ptr(), N, b.data_ptr(), None,
                                                      q.data_ptr(), None, 0, 0, 0, 0, None, None),
         }
+        if M % 256 == 0 and K % 128 == 0:
+            def pair():  # the paired Q/K launch; the second output folded into the compared one
+                rc = L.vsim_op_gemm_q4_256_pair(wq.data_ptr(), wq.data_ptr(), M, K, x.data_ptr(), N, y.data_ptr(),
+                                                y2.data_ptr(), cs.data_ptr(), 128, 64, 3, None)
+                y.view(torch.int32).bitwise_xor_(y2.view(torch.int32))
+                return rc
+            runs["q4_pair"] = pair
         for name, f in runs.items():
             out = q if name.endswith("gelu_q") or name == "q4_gelu" else y
             hip.check(f(), name)

@@ -970,10 +970,11 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
   RSk sk;
   int grid = nwg;
   const int nu = K / G2_BK / 2;
-  // (not for the V^T-copy epilogue: 167.0 vs 160.9 us per codegen-16B V GEMM with the split)
   // (grids of at least half the CUs: each tile in at most two pieces.  GPT-J-6B's 128-tile
   // GEMMs at N = 2048: prompt 32.5 -> 28.5 ms, profiles/r03_streamk_half_grid_ab.jsonl)
-  if (VSIM_STREAMK && g_streamk && !GQ && EM != 3 && nwg < SK_CUS && nwg * 2 >= SK_CUS && nu >= 2) {
+  // (the V^T-copy epilogue only below 3/4: at codegen-16B's 192 tiles 167.0 vs 160.9 us with the split)
+  if (VSIM_STREAMK && g_streamk && !GQ && (EM != 3 || nwg * 4 < SK_CUS * 3) && nwg < SK_CUS && nwg * 2 >= SK_CUS &&
+      nu >= 2) {
     const int upw = (nwg * nu + SK_CUS - 1) / SK_CUS;
     if (sk_two_pieces(nwg, nu, upw)) {
       if (int rc = sk_workspace(nwg, s, sk)) return rc;
@@ -981,7 +982,7 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
       grid = (nwg * nu + upw - 1) / upw;
     }
   }
-  if constexpr (!GQ && EM != 3) {
+  if constexpr (!GQ) {
     if (sk.upw) {
       static bool attr = false;
       if (!attr) {
