@@ -10,6 +10,7 @@
 #include "vsim_oracle.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -155,10 +156,115 @@ void parallel_rows(int nr, int nthreads, F &&fn) {
   for (auto &t : th) t.join();
 }
 
+// Work items [0, n) pulled from a shared counter by nthreads threads (the items are
+// independent, so the split changes nothing but the balance).
+template <class F>
+void parallel_items(int n, int nthreads, F &&fn) {
+  if (nthreads <= 1 || n <= 1) { for (int i = 0; i < n; ++i) fn(i); return; }
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < std::min(nthreads, n); ++t)
+    th.emplace_back([&] { for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
+  for (auto &t : th) t.join();
+}
+
+bool cpu_avx2() {
+  static const bool ok = __builtin_cpu_supports("avx2");
+  return ok;
+}
+
+typedef float v8f __attribute__((vector_size(32)));
+typedef double v4d __attribute__((vector_size(32)));
+typedef float v4f __attribute__((vector_size(16)));
+
+// The dot of imax.c:1191-1229 for 8 activation rows at once: lane t of every vector is
+// token t's own chain, with the reference's operations in the reference's order (the
+// dequantized factors d*(q-8) are the same float products, each pair term is
+// (f0*f2) + (f1*f3) rounded step by step, added to the lane's running sum; no FMA exists
+// in this target).  Only the speed of the oracle changes, not one bit of its results
+// (tests/test_oracle_golden.py holds it to the reference's goldens, prompt shapes included).
+// wf: R rows of dequantized weights [R][K]; xt: the token group's factors [K][8].
+template <int R>
+__attribute__((target("avx2"))) void dot_rows_tok8(const float *wf, int K, const float *xt, v8f *acc) {
+  v8f a[R];
+  for (int r = 0; r < R; ++r) a[r] = v8f{};
+  for (int k = 0; k < K; k += 2) {
+    v8f x0, x1;
+    std::memcpy(&x0, xt + (size_t)k * 8, 32);
+    std::memcpy(&x1, xt + (size_t)k * 8 + 8, 32);
+    for (int r = 0; r < R; ++r) {
+      const float w0 = wf[(size_t)r * K + k], w1 = wf[(size_t)r * K + k + 1];
+      a[r] = a[r] + ((w0 * x0) + (w1 * x1));
+    }
+  }
+  for (int r = 0; r < R; ++r) acc[r] = a[r];
+}
+
+// ggml.c:4891-5165 + imax.c:1182-1230 for N >= 8 activation rows: the 8-token groups go
+// through dot_rows_tok8 (4 weight rows per pass), the remaining N % 8 tokens through the
+// scalar vec_dot_q4.
+void mul_mat_q_tok8(const uint8_t *W, int M, int K, const uint8_t *xq, int N, float *y, int nthreads) {
+  const size_t rb = (size_t)K / QK * QBYTES;
+  const int nb = K / QK, G = N / 8;
+  std::vector<float> xt((size_t)G * K * 8);
+  parallel_items(G, nthreads, [&](int g) {
+    for (int t = 0; t < 8; ++t) {
+      const uint8_t *x = xq + (size_t)(8 * g + t) * rb;
+      float *o = xt.data() + (size_t)g * K * 8 + t;
+      for (int i = 0; i < nb; ++i) {
+        float d1;
+        std::memcpy(&d1, x + i * QBYTES, 4);
+        const uint8_t *p1 = x + i * QBYTES + 4;
+        for (int j = 0; j < QK / 2; ++j) {
+          const uint8_t v1 = p1[j];
+          o[(size_t)(i * QK + 2 * j) * 8] = d1 * ((int8_t)(v1 & 0xf) - 8);
+          o[(size_t)(i * QK + 2 * j + 1) * 8] = d1 * ((int8_t)(v1 >> 4) - 8);
+        }
+      }
+    }
+  });
+  constexpr int R = 4;
+  const int nblk = (M + R - 1) / R;
+  parallel_items(nblk, nthreads, [&](int blk) {
+    const int r0 = blk * R, nr = std::min(R, M - r0);
+    std::vector<float> wf((size_t)R * K);
+    for (int r = 0; r < nr; ++r) {  // f0 = d0*(q-8) as imax.c:1203-1206
+      const uint8_t *w = W + (size_t)(r0 + r) * rb;
+      for (int i = 0; i < nb; ++i) {
+        float d0;
+        std::memcpy(&d0, w + i * QBYTES, 4);
+        const uint8_t *p0 = w + i * QBYTES + 4;
+        for (int j = 0; j < QK / 2; ++j) {
+          const uint8_t v0 = p0[j];
+          wf[(size_t)r * K + i * QK + 2 * j] = d0 * ((int8_t)(v0 & 0xf) - 8);
+          wf[(size_t)r * K + i * QK + 2 * j + 1] = d0 * ((int8_t)(v0 >> 4) - 8);
+        }
+      }
+    }
+    for (int g = 0; g < G; ++g) {
+      v8f acc[R];
+      const float *xg = xt.data() + (size_t)g * K * 8;
+      if (nr == R) {
+        dot_rows_tok8<R>(wf.data(), K, xg, acc);
+      } else {
+        for (int r = 0; r < nr; ++r) dot_rows_tok8<1>(wf.data() + (size_t)r * K, K, xg, acc + r);
+      }
+      for (int r = 0; r < nr; ++r)
+        for (int t = 0; t < 8; ++t) y[(size_t)(8 * g + t) * M + r0 + r] = acc[r][t];
+    }
+    for (int ic = 8 * G; ic < N; ++ic)
+      for (int r = 0; r < nr; ++r) y[(size_t)ic * M + r0 + r] = vec_dot_q4(K, W + (size_t)(r0 + r) * rb, xq + ic * rb);
+  });
+}
+
 // ggml.c:4891-5165 + imax.c:1182-1230: dst[ic*M + ir] = dot(W row ir, xq row ic).
 // Rows are independent chains, so the result does not depend on nthreads.
 void mul_mat_q(const uint8_t *W, int M, int K, const uint8_t *xq, int N, float *y, int nthreads) {
   const size_t rb = (size_t)K / QK * QBYTES;
+  if (N >= 8 && cpu_avx2()) {
+    mul_mat_q_tok8(W, M, K, xq, N, y, nthreads);
+    return;
+  }
   parallel_rows(M, nthreads, [&](int r0, int r1) {
     for (int ir = r0; ir < r1; ++ir)
       for (int ic = 0; ic < N; ++ic) y[(size_t)ic * M + ir] = vec_dot_q4(K, W + ir * rb, xq + ic * rb);
@@ -168,7 +274,8 @@ void mul_mat_q(const uint8_t *W, int M, int K, const uint8_t *xq, int N, float *
 void mul_mat_f(const uint8_t *W, int M, int K, const float *x, int N, float *y, int nthreads) {
   const size_t rb = (size_t)K / QK * QBYTES;
   std::vector<uint8_t> wdata(rb * N);  // INIT phase, ggml.c:5024-5041
-  for (int ic = 0; ic < N; ++ic) quantize_row(x + (size_t)ic * K, wdata.data() + ic * rb, K);
+  parallel_items(N, N >= 64 ? nthreads : 1,
+                 [&](int ic) { quantize_row(x + (size_t)ic * K, wdata.data() + ic * rb, K); });
   mul_mat_q(W, M, K, wdata.data(), N, y, nthreads);
 }
 
@@ -248,32 +355,66 @@ void rope_gptj(float *x, int d, int H, int T, int n_past, int n_dims, int mode) 
   }
 }
 
-// ggml.c:4495-4534 (non-transposed src0) + ggml_vec_dot_f32 ggml.c:399-434
-void kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int N, float *out) {
-  for (int h = 0; h < H; ++h)
+// ggml.c:4495-4534 (non-transposed src0) + ggml_vec_dot_f32 ggml.c:399-434: per (head, key,
+// query) sumf += x[i]*y[i] in double (float products), cast to float.  For 8 or more queries
+// the queries of a head go 8 at a time through vectors (lane q = query q's own sum, same order);
+// heads run on nthreads threads.
+__attribute__((target("avx2"))) void kq_head_q8(const float *K, int ldk, const float *Qt, int d, int nk, int nq8,
+                                                float *out, int N) {
+  for (int k = 0; k < nk; ++k) {
+    const float *kr = K + (size_t)k * ldk;
+    for (int g = 0; g < nq8; ++g) {
+      v4d s0{}, s1{};
+      const float *qg = Qt + (size_t)g * d * 8;
+      for (int i = 0; i < d; ++i) {
+        v8f qv;
+        std::memcpy(&qv, qg + (size_t)i * 8, 32);
+        const v8f pr = kr[i] * qv;
+        const v4f lo = {pr[0], pr[1], pr[2], pr[3]}, hi = {pr[4], pr[5], pr[6], pr[7]};
+        s0 = s0 + __builtin_convertvector(lo, v4d);
+        s1 = s1 + __builtin_convertvector(hi, v4d);
+      }
+      for (int t = 0; t < 4; ++t) out[(size_t)(8 * g + t) * nk + k] = (float)s0[t];
+      for (int t = 0; t < 4; ++t) out[(size_t)(8 * g + 4 + t) * nk + k] = (float)s1[t];
+    }
+  }
+  (void)N;
+}
+
+void kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int N, float *out, int nthreads = 1) {
+  const int nq8 = cpu_avx2() ? N / 8 : 0;
+  parallel_items(H, nthreads, [&](int h) {
+    if (nq8) {
+      std::vector<float> Qt((size_t)nq8 * d * 8);  // [group][i][8]
+      for (int q = 0; q < 8 * nq8; ++q)
+        for (int i = 0; i < d; ++i) Qt[((size_t)(q / 8) * d + i) * 8 + q % 8] = Q[(size_t)q * ldq + h * d + i];
+      kq_head_q8(K + h * d, ldk, Qt.data(), d, nk, nq8, out + (size_t)h * N * nk, N);
+    }
     for (int k = 0; k < nk; ++k)
-      for (int q = 0; q < N; ++q) {
+      for (int q = 8 * nq8; q < N; ++q) {
         const float *kr = K + (size_t)k * ldk + h * d;
         const float *qr = Q + (size_t)q * ldq + h * d;
         double sumf = 0.0;
         for (int i = 0; i < d; ++i) sumf += kr[i] * qr[i];
         out[((size_t)h * N + q) * nk + k] = (float)sumf;
       }
+  });
 }
 
-// ggml.c:4535-4581 (transposed src0, nth == 1) + ggml_vec_mad_f32 ggml.c:610-639
-void kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int N, float *out) {
-  for (int h = 0; h < H; ++h)
-    for (int q = 0; q < N; ++q) {
-      float *y = out + ((size_t)h * N + q) * d;
-      for (int i = 0; i < d; ++i) y[i] = 0.0f;
-      const float *srow = S + ((size_t)h * N + q) * nk;
-      for (int k = 0; k < nk; ++k) {
-        const float v = srow[k];
-        const float *x = V + (size_t)k * ldv + h * d;
-        for (int i = 0; i < d; ++i) y[i] += x[i] * v;
-      }
+// ggml.c:4535-4581 (transposed src0, nth == 1) + ggml_vec_mad_f32 ggml.c:610-639; the
+// (head, query) rows are independent and run on nthreads threads
+void kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int N, float *out, int nthreads = 1) {
+  parallel_items(H * N, H * N >= 64 ? nthreads : 1, [&](int hq) {
+    const int h = hq / N, q = hq % N;
+    float *y = out + ((size_t)h * N + q) * d;
+    for (int i = 0; i < d; ++i) y[i] = 0.0f;
+    const float *srow = S + ((size_t)h * N + q) * nk;
+    for (int k = 0; k < nk; ++k) {
+      const float v = srow[k];
+      const float *x = V + (size_t)k * ldv + h * d;
+      for (int i = 0; i < d; ++i) y[i] += x[i] * v;
     }
+  });
 }
 
 // ggml.c:6184-6244 ggml_compute_forward_alibi_f32 on p[nz][nr][nc] (ne0 = nc keys, ne1 = nr
@@ -521,7 +662,7 @@ void eval_bloom(Model &m, int n_past, const int32_t *tok, int N, float *logits, 
       std::memcpy(mk + (size_t)(n_past + t) * E, qkv.data() + (size_t)t * 3 * E + E, sizeof(float) * E);
       std::memcpy(mv + (size_t)(n_past + t) * E, qkv.data() + (size_t)t * 3 * E + 2 * E, sizeof(float) * E);
     }
-    kq(mk, E, Q.data(), E, d, H, nk, N, KQ.data());
+    kq(mk, E, Q.data(), E, d, H, nk, N, KQ.data(), nthreads);
     for (auto &v : KQ) v *= scale;
     alibi(KQ.data(), nk, N, H, H);
     for (int h = 0; h < H; ++h)
@@ -529,7 +670,7 @@ void eval_bloom(Model &m, int n_past, const int32_t *tok, int N, float *logits, 
         for (int i = n_past; i < nk; ++i)
           if (i > n_past + j) KQ[((size_t)h * N + j) * nk + i] = -INFINITY;
     for (int r = 0; r < H * N; ++r) soft_max_row(KQ.data() + (size_t)r * nk, nk);
-    kqv(mv, E, KQ.data(), d, H, nk, N, KQV.data());
+    kqv(mv, E, KQ.data(), d, H, nk, N, KQV.data(), nthreads);
     for (int t = 0; t < N; ++t)
       for (int h = 0; h < H; ++h)
         for (int i = 0; i < d; ++i) cur[(size_t)t * E + h * d + i] = KQV[((size_t)h * N + t) * d + i];
@@ -547,9 +688,9 @@ void eval_bloom(Model &m, int n_past, const int32_t *tok, int N, float *logits, 
   }
   for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
   affine(cur, m.lnf_w, m.lnf_b, E, N);
-  std::vector<float> lg((size_t)V * N);
-  mul_mat_f(m.lmh.data(), V, E, cur.data(), N, lg.data(), nthreads);
-  std::memcpy(logits, lg.data() + (size_t)V * (N - 1), sizeof(float) * V);
+  std::vector<float> lg((size_t)V);  // the last row only, as in eval()
+  mul_mat_f(m.lmh.data(), V, E, cur.data() + (size_t)E * (N - 1), 1, lg.data(), nthreads);
+  std::memcpy(logits, lg.data(), sizeof(float) * V);
 }
 
 // vsim.cpp:470-747 (GPT-NeoX) ; the GPT-J graph is the same op sequence with ggml_rope
@@ -594,14 +735,17 @@ void eval(Model &m, int n_past, const int32_t *tok, int N, float *logits, int nt
       rope_neox(Q.data(), d, H, N, n_past, m.n_rot, 0);
       rope_neox(mk, d, H, nk, n_past, m.n_rot, 1);
     }
-    kq(mk, E, Q.data(), E, d, H, nk, N, KQ.data());
-    for (auto &v : KQ) v *= scale;
-    for (int h = 0; h < H; ++h)
-      for (int j = 0; j < N; ++j)
-        for (int i = n_past; i < nk; ++i)
-          if (i > n_past + j) KQ[((size_t)h * N + j) * nk + i] = -INFINITY;
-    for (int r = 0; r < H * N; ++r) soft_max_row(KQ.data() + (size_t)r * nk, nk);
-    kqv(mv, E, KQ.data(), d, H, nk, N, KQV.data());
+    kq(mk, E, Q.data(), E, d, H, nk, N, KQ.data(), nthreads);
+    // scale, diag_mask_inf, soft_max: row by row (each row's ops are the reference's)
+    parallel_items(H * N, H * N >= 64 ? nthreads : 1, [&](int r) {
+      float *row = KQ.data() + (size_t)r * nk;
+      const int j = r % N;
+      for (int i = 0; i < nk; ++i) row[i] *= scale;
+      for (int i = n_past; i < nk; ++i)
+        if (i > n_past + j) row[i] = -INFINITY;
+      soft_max_row(row, nk);
+    });
+    kqv(mv, E, KQ.data(), d, H, nk, N, KQV.data(), nthreads);
     for (int t = 0; t < N; ++t)
       for (int h = 0; h < H; ++h)
         for (int i = 0; i < d; ++i) cur[(size_t)t * E + h * d + i] = KQV[((size_t)h * N + t) * d + i];
@@ -636,11 +780,13 @@ void eval(Model &m, int n_past, const int32_t *tok, int N, float *logits, int nt
   }
   for (int t = 0; t < N; ++t) norm_row(inpL.data() + (size_t)t * E, cur.data() + (size_t)t * E, E);
   affine(cur, m.lnf_w, m.lnf_b, E, N);
-  // lm_head over all N rows (vsim.cpp:716-718); only the last row is returned
-  std::vector<float> lg((size_t)V * N);
-  mul_mat_f(m.lmh.data(), V, E, cur.data(), N, lg.data(), nthreads);
-  if (gptj) add_bias(lg, m.lmh_b, V, N);
-  std::memcpy(logits, lg.data() + (size_t)V * (N - 1), sizeof(float) * V);
+  // lm_head (vsim.cpp:716-718) runs over all N rows and only the last row is returned
+  // (vsim.cpp:736-737); every output row is its own chains over its own activation row, so
+  // the last row alone gives the same bits
+  std::vector<float> lg((size_t)V);
+  mul_mat_f(m.lmh.data(), V, E, cur.data() + (size_t)E * (N - 1), 1, lg.data(), nthreads);
+  if (gptj) add_bias(lg, m.lmh_b, V, 1);
+  std::memcpy(logits, lg.data(), sizeof(float) * V);
 }
 
 // utils.cpp:339-422 sample_top_p_top_k_repeat_penalty
