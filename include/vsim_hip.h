@@ -173,6 +173,9 @@ int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, cons
 /* cumulative counts of exact-LayerNorm rows that needed the sequential fallback:
  * out[0] = mean not certified, out[1] = variance scale not certified (device-wide) */
 int vsim_norm_fallbacks(unsigned out[2]);
+/* cumulative count of bounded cross-workgroup waits that gave up (the fused layer tail's wait for
+ * its attention heads; placement-independent by construction, so 0 in every healthy run) */
+int vsim_spin_timeouts(unsigned *out);
 int vsim_op_gelu(const float *x, float *y, int n, void *stream);
 /* scale -> diag_mask_inf(n_past) -> soft_max over p[nz][nr][nc], in place */
 int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream);

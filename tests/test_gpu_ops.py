@@ -86,6 +86,26 @@ def test_gemv_exact_bit_exact(c):
     assert np.array_equal(bits(y), bits(c["y"]))
 
 
+@pytest.mark.parametrize("M,K,N", [(33, 64, 2), (130, 96, 129), (1000, 128, 300), (257, 4096, 5),
+                                   (4096, 64, 1030), (6144, 256, 256), (96, 24576, 17)])
+def test_gemm_exact_ragged_vs_oracle(M, K, N):
+    """The exact prompt GEMM (gemm_exact.hip: 128 x 128 tiles of (row, token) chains) against
+    the oracle's mul_mat (ggml.c:4891-5165 with its INIT quantization): bit-identical at ragged
+    M, N (partial tiles in both directions), one-block K, and with a bias epilogue."""
+    import oracle_py as O
+    rng = np.random.default_rng(M * 7 + K * 3 + N)
+    w_aos = mg.quantize_q4_0(rng.standard_normal(M * K).astype(np.float32) * np.float32(0.02))
+    x = (rng.standard_normal(N * K) * 1.5).astype(np.float32)
+    w = repack(w_aos, M, K)
+    xq, xd = quantize(x, K, N)
+    y = gemv(w, M, K, xq, xd, N, hip.MODE_EXACT).reshape(N, M)
+    y_or = O.mul_mat(w_aos, M, K, x, N, nthreads=8).reshape(N, M)
+    assert np.array_equal(bits(y), bits(y_or))
+    b = rng.standard_normal(M).astype(np.float32)
+    yb = gemv(w, M, K, xq, xd, N, hip.MODE_EXACT, bias=dev(b)).reshape(N, M)
+    assert np.array_equal(bits(yb), bits(y_or + b[None, :]))
+
+
 def _fp64_product(w_aos, M, K, xq_aos, N):
     W = mg.dequantize_q4_0(w_aos, K).astype(np.float64)       # [M, K]
     X = mg.dequantize_q4_0(xq_aos, K).astype(np.float64)      # [N, K]
@@ -243,6 +263,30 @@ def test_kqv_bit_exact():
         assert np.array_equal(bits(host(out)), bits(c["y"])), c["shape"]
 
 
+@pytest.mark.parametrize("d,H,nk,N", [(64, 3, 130, 70), (96, 2, 97, 33), (256, 2, 300, 257), (4, 1, 5, 3),
+                                      (128, 2, 64, 64)])
+def test_kq_kqv_tiled_vs_oracle(d, H, nk, N):
+    """The prompt attention products (attn_exact.hip, 64 x 64 register tiles) against the
+    oracle's KQ (double sum of float products, ggml.c:399-434) and KQV (float chain over the keys,
+    ggml.c:610-639) at ragged shapes: partial tiles in every direction, d not a multiple of the
+    32-element staging chunk, softmax-like rows with exact zeros."""
+    import oracle_py as O
+    rng = np.random.default_rng(d * 1000 + nk + N)
+    K = rng.standard_normal((nk, d * H)).astype(np.float32)
+    Q = rng.standard_normal((N, d * H)).astype(np.float32)
+    out = torch.empty(H * N * nk, dtype=torch.float32, device=DEV)
+    Kd, Qd = dev(K), dev(Q)  # (held: a temporary's memory would be reused by the next allocation)
+    hip.check(hip.lib().vsim_op_kq(Kd.data_ptr(), d * H, Qd.data_ptr(), d * H, d, H, nk, N, out.data_ptr(), None), "kq")
+    assert np.array_equal(bits(host(out)), bits(O.kq(K, Q, d, H, nk, N)))
+    V = rng.standard_normal((nk, d * H)).astype(np.float32)
+    S = rng.random((H, N, nk)).astype(np.float32)
+    S[S < 0.3] = 0.0
+    out = torch.empty(H * N * d, dtype=torch.float32, device=DEV)
+    Vd, Sd = dev(V), dev(S)
+    hip.check(hip.lib().vsim_op_kqv(Vd.data_ptr(), d * H, Sd.data_ptr(), d, H, nk, N, out.data_ptr(), None), "kqv")
+    assert np.array_equal(bits(host(out)), bits(O.kqv(V, S, d, H, nk, N)))
+
+
 def test_get_rows_bit_exact():
     z = ops("getrows")
     K, V = (int(v) for v in z["shape"])
@@ -346,7 +390,8 @@ def test_prompt_gemm_vs_reference_mul_mat(c):
     assert np.array_equal(bits(y), bits(y_ref)), "exact prompt GEMV"
     # the fast path, as the model's long-prompt layer calls it (the GEMM on the W4T32 weight)
     x16 = torch.empty(N * K, dtype=torch.float16, device=DEV)
-    hip.check(hip.lib().vsim_op_act_quant_f16(dev(x).data_ptr(), K, N, None, 0, x16.data_ptr(), None), "act_quant")
+    xt = dev(x)
+    hip.check(hip.lib().vsim_op_act_quant_f16(xt.data_ptr(), K, N, None, 0, x16.data_ptr(), None), "act_quant")
     yf = torch.empty(N * M, dtype=torch.float32, device=DEV)
     hip.check(hip.lib().vsim_op_gemm_q4_256(w.data_ptr(), M, K, x16.data_ptr(), N, None, yf.data_ptr(), None, None,
                                             0, 0, 0, 0, None, None), "gemm")
@@ -385,7 +430,8 @@ def test_prefill_gemm_f16_256(M, K, N):
     X16 = (rng.standard_normal((N, K)) * 0.5).astype(np.float16)
     x16 = torch.from_numpy(X16).to(DEV)
     y = torch.empty(N * M, dtype=torch.float32, device=DEV)
-    hip.check(hip.lib().vsim_op_gemm_f16(img.data_ptr(), M, K, x16.data_ptr(), N, dev(b).data_ptr(), y.data_ptr(),
+    bt = dev(b)
+    hip.check(hip.lib().vsim_op_gemm_f16(img.data_ptr(), M, K, x16.data_ptr(), N, bt.data_ptr(), y.data_ptr(),
                                          None), "gemm")
     torch.cuda.synchronize()
     y = y.cpu().numpy().reshape(N, M)

@@ -159,52 +159,18 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
       *(u32x4 *)&Vt[(c8 / 8) * VLD + 8 * (c8 % 8)] = rv[c];
     }
   };
-  // D = 256 (GL): the register ring of the next tile does not fit beside the 256-dim Q
-  // fragments and O^T accumulators, so the tiles go by LDS-DMA into two unpadded LDS buffers
-  // (16-byte chunks XOR-swizzled on the DMA's source address: K rows by row & 15, V^T rows by
-  // (row >> 1) & 7), the next tile in flight during this one's MFMAs; retired by vmcnt(0) before
-  // the step's closing barrier.
-  constexpr bool GL = D == 256;
-  constexpr bool PF = !GL;
-  const uint32_t lb = lds_addr(lds);
-  const int wv = __builtin_amdgcn_readfirstlane(wave);  // (the DMA's LDS address goes to M0)
-  auto gl_stage = [&](int kb, int buf) __attribute__((always_inline)) {
-    const int k0 = kb * AP_BK;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {  // K: 2 rows (keys) per wave instruction
-      const int row0 = (j * 4 + wv) * 2, row = row0 + (lane >> 5);
-      const int c = (lane & 31) ^ (row & 15);
-      glds16<false>(kbase + (size_t)min(k0 + row, klast) * E + 8 * c,
-                    lb + (uint32_t)((buf * AP_BK * D + row0 * D) * 2));
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {  // V^T: 8 rows (dims) per wave instruction
-      const int row0 = (j * 4 + wv) * 8, row = row0 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      glds16<false>(vbase + (size_t)row * ldt + k0 + 8 * c,
-                    lb + (uint32_t)((2 * AP_BK * D + buf * D * AP_BK + row0 * AP_BK) * 2));
-    }
-  };
-  if (GL) {
-    gl_stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (PF) {
-    kload(0);
-    vload(0);
-    kstore(0);
-    vstore(0);
-    __syncthreads();
-  }
+  kload(0);
+  vload(0);
+  kstore(0);
+  vstore(0);
+  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * AP_BK, buf = kb & 1;
-    const bool next = PF && kb + 1 < nkb;
-    if (GL && kb + 1 < nkb) gl_stage(kb + 1, buf ^ 1);
+    const bool next = kb + 1 < nkb;
     // next tile: K rows load during this tile's S^T, V^T rows during its P·V
     if (next) kload(kb + 1);
-    const _Float16 *Ks = GL ? lds + buf * AP_BK * D : lds + buf * AP_BK * KLD;
-    const _Float16 *Vt = GL ? lds + 2 * AP_BK * D + buf * D * AP_BK : lds + 2 * AP_BK * KLD + buf * D * VLD;
+    const _Float16 *Ks = lds + buf * AP_BK * KLD;
+    const _Float16 *Vt = lds + 2 * AP_BK * KLD + buf * D * VLD;
     const bool vis = k0 <= n_past + min(qw + 31, N - 1);  // wave-uniform: some key of the block is visible
     af32x16 st[2];
     if (vis) {
@@ -215,12 +181,10 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
           const int krow = 32 * t + r;
-          const ahalf8 kf = GL ? *(const ahalf8 *)&Ks[krow * D + 8 * ((2 * s + hl) ^ (krow & 15))]
-                               : *(const ahalf8 *)&Ks[krow * KLD + 16 * s + 8 * hl];
+          const ahalf8 kf = *(const ahalf8 *)&Ks[krow * KLD + 16 * s + 8 * hl];
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st[t], 0, 0, 0);
           // (a scheduling fence every 4 steps: the compiler would otherwise hoist all the
           // tile's LDS reads and run out of registers at D = 256)
-          if (D >= 256 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
@@ -269,15 +233,12 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
           for (int i = 0; i < NT; ++i) {
             const int vrow = 32 * i + r, vc = kbase2 >> 3;  // (kbase2 & 7 == 4 hl: within the chunk)
             // (vt_pos order: the lane's keys kbase2 .. +3 and kbase2 + 8 .. +11 are chunk vc + hl)
-            const ahalf8 vf = GL ? *(const ahalf8 *)&Vt[vrow * AP_BK + 8 * ((vc + hl) ^ ((vrow >> 1) & 7))]
-                                 : *(const ahalf8 *)&Vt[vrow * VLD + 8 * (vc + hl)];
+            const ahalf8 vf = *(const ahalf8 *)&Vt[vrow * VLD + 8 * (vc + hl)];
             o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
-            if (D >= 256 && (i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
           }
         }
     }
     if (next) vstore(buf ^ 1);
-    if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile has landed
     __syncthreads();
   }
   // O^T / l: lane = query, rows = dims (reg & 3) + 8 (reg >> 2) + 4 hl of tile i
@@ -309,12 +270,7 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
 // Each wave keeps the running sum of its own keys' probabilities; the two partial sums are
 // added (half 0's first) at the end.  ≈190 registers: two waves per SIMD.  Barriers per key
 // block: after the maxima, after the P^T stores, after the next tile's DMA (as above).
-#ifndef AP_KPF  // K fragments in flight in the S^T chain (A/B builds)
-#define AP_KPF 4
-#endif
-#ifndef VSIM_AP_STAGGER  // (A/B builds: 0 runs both wave groups in the same phase)
-#define VSIM_AP_STAGGER 1
-#endif
+constexpr int AP_KPF = 4;  // K fragments in flight in the S^T chain
 constexpr int AP2_THREADS = 512;
 constexpr size_t ap2_lds() { return (size_t)2 * 2 * AP_BK * 256 * sizeof(_Float16) + 4 * 2 * 2 * 64 * 16 + 4 * 2 * 64 * 4; }
 
@@ -334,10 +290,10 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
   const int h = blockIdx.x % H, q0 = (nqb - 1 - (int)blockIdx.x / H) * AP_BQ;
   const int tid = threadIdx.x, lane = tid & 63;
   // pair (2 g, 2 g + 1) takes query group g; groups 0, 1 (waves 0-3, one per SIMD) lead, groups
-  // 2, 3 (waves 4-7) run one barrier behind (VSIM_AP_STAGGER), so the two waves on a SIMD are
+  // 2, 3 (waves 4-7) run one barrier behind, so the two waves on a SIMD are
   // in different phases: one's softmax beside the other's MFMAs
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wv >> 1, half = wv & 1;
-  const bool lag = VSIM_AP_STAGGER && wv >= 4;
+  const bool lag = wv >= 4;
   const int r = lane & 31, hl = lane >> 5;
   const int qw = q0 + grp * 32;
   const int myq = qw + r;
@@ -498,7 +454,7 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
     }
     __syncthreads();
   }
-  if (VSIM_AP_STAGGER && !lag) __builtin_amdgcn_s_barrier();  // (pairs with the lagging group's last)
+  if (!lag) __builtin_amdgcn_s_barrier();  // (pairs with the lagging group's last)
   // the running sums of both halves (half 0's + half 1's, in that order, in both waves)
   mex[(grp * 2 + half) * 64 + lane] = lrow;
   __syncthreads();
@@ -547,17 +503,11 @@ __global__ void __launch_bounds__(AP2_THREADS, 1) k_attn_prefill_pair(const floa
 }
 
 bool attn_prefill_supported(int d) { return d == 64 || d == 96 || d == 128 || d == 256; }
-#ifndef VSIM_ATTN_PAIR  // (A/B builds: 0 keeps D = 256 on the one-wave-per-group kernel)
-#define VSIM_ATTN_PAIR 1
-#endif
-#ifndef VSIM_ATTN_Q16  // 0: the out-projection's fp16 operand made by a separate quantization pass (A/B)
-#define VSIM_ATTN_Q16 1
-#endif
-bool attn_prefill_quantizes(int d) { return VSIM_ATTN_PAIR && VSIM_ATTN_Q16 && d == 256; }
+// (head dim 256: the two-wave kernel, which also writes the out-projection's fp16 operand)
+bool attn_prefill_quantizes(int d) { return d == 256; }
 
 template <int D>
 size_t attn_prefill_lds() {
-  if (D == 256) return (size_t)2 * 2 * AP_BK * D * sizeof(_Float16);  // K and V^T, two buffers each, unpadded
   return (size_t)(2 * AP_BK * (D + 8) + 2 * D * (AP_BK + 8)) * sizeof(_Float16);
 }
 
@@ -598,13 +548,7 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
     hipLaunchKernelGGL(k_kv_f16, dim3(ldt / 64, E / 64), dim3(256), 0, s, kc, vc, E, d, nk, ldt, k16, vt16, f0, f1);
   const float qscale = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
   const dim3 grid(((N + AP_BQ - 1) / AP_BQ) * H);
-  static bool attr = false;
-  if (!attr) {
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_attn_prefill_f16<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)attn_prefill_lds<256>()));
-    attr = true;
-  }
-  if (VSIM_ATTN_PAIR && d == 256) {
+  if (d == 256) {
     static bool attr2 = false;
     if (!attr2) {
       VSIM_HIP(hipFuncSetAttribute((const void *)k_attn_prefill_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -623,8 +567,7 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
   switch (d) {
     case 64: APL(64); break;
     case 96: APL(96); break;
-    case 128: APL(128); break;
-    default: APL(256); break;
+    default: APL(128); break;
   }
 #undef APL
   VSIM_HIP(hipGetLastError());

@@ -112,6 +112,7 @@ int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, fl
   return launch_get_rows(w, K, V, rows, n, y, (hipStream_t)stream);
 }
 int vsim_norm_fallbacks(unsigned out[2]) { return vsim::norm_stats(out); }
+int vsim_spin_timeouts(unsigned *out) { return vsim::spin_timeouts(out); }
 
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream) {
   return launch_norm(x, y, k, rows, w, b, (hipStream_t)stream);

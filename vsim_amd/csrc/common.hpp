@@ -251,7 +251,9 @@ struct DevTables {
   const uint16_t *gelu_f16;  // table_gelu_f16 (ggml.c:1247)
 };
 int tables_get(DevTables *t);
-int norm_stats(unsigned *out2);  // LayerNorm fallback counters (ops_elt.hip)  // lazily uploads host-built tables for the current device
+int norm_stats(unsigned *out2);
+unsigned *spin_error_counter();  // device counter of bounded waits that gave up (null before tables_get)
+int spin_timeouts(unsigned *out);  // LayerNorm fallback counters (ops_elt.hip)  // lazily uploads host-built tables for the current device
 
 int launch_q4_repack(const void *aos, void *soa, int rows, int k, hipStream_t s);
 int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s);
@@ -259,6 +261,8 @@ int launch_q4_quantize(const float *x, int k, int n, void *xq, float *xd, hipStr
 int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd, int n, const float *bias,
                    float *y, int mode, hipStream_t s);
 int launch_gemv_batch(const GemvBatch &B, int mode, hipStream_t s);
+// exact mode, N > 1 tokens: every (row, token) the reference's fp32 chain (gemm_exact.hip)
+int launch_gemm_exact(const W4 &W, const float *xd, int n, const float *bias, float *y, hipStream_t s);
 int launch_act_repack(const void *aos, void *xq, int n, int k, hipStream_t s);
 int launch_act_unpack(const void *xq, void *aos, int n, int k, hipStream_t s);
 int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s);
@@ -276,10 +280,7 @@ int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool g
 int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s);
 // long prompts: fp16 weight images (launch_w4_expand_f16: [M][K], 2 bytes per weight) and the
 // 256 x 256-tile GEMM on them (K % 64 == 0), same operand values as launch_gemm_f16x
-#ifndef VSIM_G2_MIN_N  // (A/B builds: tools/variant.sh with -DVSIM_G2_MIN_N=...)
-#define VSIM_G2_MIN_N 256
-#endif
-constexpr int G2_MIN_N = VSIM_G2_MIN_N;
+constexpr int G2_MIN_N = 256;
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
 // q16 non-null: y is not written; bias + GELU + Q4_0 quantize of the result into q16 ([n][M]
 // fp16 values d*(q-8), the next GEMM's operand, as launch_act_quant_f16(y, ..., gelu) makes)
@@ -316,7 +317,8 @@ int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, 
                             const G2Epi &e1, hipStream_t s);
 bool gemm_pair_enabled(int M, int K);
 int gemm_set_qk_pair(int mode);  // vsim_gemm_set_qk_pair (0 off, 1 default, 2 no split); returns the old setting
-int gemm_set_streamk(int on);  // stream-K split of the register-dequant GEMM (default on); returns the old setting
+int gemm_set_streamk(int on);
+int gemm_release_stream(hipStream_t s);  // frees the stream-K workspace of (current device, s)  // stream-K split of the register-dequant GEMM (default on); returns the old setting
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call); fresh: the new keys [n_past, n_past + N) are
@@ -342,10 +344,13 @@ int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scal
 void alibi_slopes_host(float *m, int n_head);
 int launch_rope(int style, float *x, int d, int H, int T, int n_past, int n_dims, int mode,
                 const double2 *cs, hipStream_t s);
+// exact KQ / KQV of a batch of n queries over nk keys (attn_exact.hip); n_past >= 0: the causal
+// mask of the prompt follows (query j sees keys <= n_past + j): fully masked KQ tiles are left
+// unwritten, KQV stops at the last unmasked key.  merged = 1: out [n][H d], else [H][n][d]
 int launch_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq,
-              hipStream_t s);
+              hipStream_t s, int n_past = -1);
 int launch_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, int merged,
-               hipStream_t s);
+               hipStream_t s, int n_past = -1);
 int launch_rope_kv_write(int style, float *Q, const float *K, const float *V, float *kcache, float *vcache,
                          int d, int H, int N, int n_past, int n_dims, const double2 *cs, hipStream_t s);
 int launch_add_residual(float *inpL, const float *attn, const float *ff, int n, int order_ff_first,

@@ -673,19 +673,22 @@ constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
 // Stream-K (sk.upw > 0, for grids of fewer tiles than CUs: the 192 tiles of every 6144-row
 // codegen-16B GEMM): the grid is one workgroup per CU and workgroup b takes the K-tile pairs
 // ("units") [b upw, (b + 1) upw) of the tiles laid end to end, so every CU does the same work.
-// A tile split between two workgroups: the one holding its start (the lower index) computes that
-// part first thing and publishes its accumulators (write-through sc1 stores in the register
-// layout, drained, then an sc1 flag holding this launch's epoch); the one holding its end
-// computes that part last, polls the flag (sc1), adds the partial with sc1 loads (one rounded
-// add per value: partial + own, the same in every run) and runs the epilogue.  Waits only on
-// lower-indexed workgroups, dispatched before it; the launcher checks no tile has 3 pieces.
+// A tile split between two workgroups has a start piece (K from 0) and an end piece.  Nobody
+// waits for anybody (no assumption on dispatch order or co-residence): each piece counts its
+// arrival on the tile's counter (agent-scope atomic), and whichever arrives second adds the
+// other's partial (partial_start + partial_end, one rounded add per value: the same bits
+// whichever piece finishes) and runs the epilogue, then clears the counter for the next launch.
+//  * the start piece (computed first) always publishes its partial (write-through sc1 stores in
+//    the register layout, drained) before it counts;
+//  * the end piece (computed last) first looks at the counter: when the start has arrived (the
+//    usual case) it finishes without publishing; otherwise it publishes its own partial, counts,
+//    and finishes only if the start arrived in between.
 // Hybrid split (PAIR launches, wg0 > 0): workgroups [0, wg0) take the whole tiles [0, wg0) (a
 // full round of the CUs), the rest run the split above over the tiles from t0 = wg0 on.
 struct RSk {
-  int upw = 0;          // units (K-tile pairs) per workgroup; 0: one tile per workgroup
-  float *ws = nullptr;  // partials: [tile - t0][wave][32 f32x4][64 lanes]
-  unsigned *flags = nullptr;
-  unsigned epoch = 0;
+  int upw = 0;           // units (K-tile pairs) per workgroup; 0: one tile per workgroup
+  float *ws = nullptr;   // partials: [tile - t0][piece: 0 start, 1 end][wave][32 f32x4][64 lanes]
+  unsigned *cnt = nullptr;  // arrivals per split tile (0 between launches)
   int wg0 = 0, t0 = 0;
 };
 
@@ -850,12 +853,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     const int u0 = ((int)blockIdx.x - (PAIR ? sk.wg0 : 0)) * sk.upw, u1 = min(u0 + sk.upw, (nwg - t0) * nu);
     const int tA = u0 / nu, aA = u0 - tA * nu, eA = min(u1 - tA * nu, nu);
     const int eB = max(u1 - (tA + 1) * nu, 0);  // units of tA + 1 from its start
-    // first: the piece that starts a tile and is finished by the next workgroup (published)
-    const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
-    if (pubA || pubB) {
-      const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
-      run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 0, 2 * e);
-      float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
+    __shared__ unsigned sk_arrived;
+    auto slot = [&](int t, int piece) { return sk.ws + ((size_t)((2 * t + piece) * 8 + wave) * 32 * 64 + lane) * 4; };
+    auto publish = [&](float *wp) __attribute__((always_inline)) {
       // (4 stores per base address, offsets 0-3 KB)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -872,21 +872,16 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(sk.flags + t, sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (pubA) return;  // (tA's start was the whole range)
-    }
-    // then the piece this workgroup finishes: tA from aA (after a published tA + 1 start), or
-    // tA + 1 whole / tA whole
-    const bool finA = !pubA;
-    const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
-    if (!finA && e < nu) return;
-    run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 2 * a, 2 * (e - a));
-    if (a > 0) {  // the earlier part's partial
-      if (tid == 0)
-        while (__hip_atomic_load(sk.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sk.epoch)
-          __builtin_amdgcn_s_sleep(2);
+    };
+    // this piece's arrival on tile t's counter; true when it is the second (it finishes)
+    auto arrive = [&](int t) __attribute__((always_inline)) -> bool {
+      if (tid == 0) sk_arrived = __hip_atomic_fetch_add(sk.cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      const float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
+      return sk_arrived != 0;
+    };
+    // acc = partial_start + partial_end, `other` the piece not in acc; the counter cleared
+    auto combine = [&](int t, const float *wp, bool other_is_start) __attribute__((always_inline)) {
+      if (tid == 0) __hip_atomic_store(sk.cnt + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int g = 0; g < 8; ++g) {  // 4 registers' worth at a time (acc holds 128 VGPRs)
         f32x4 pv[4];
@@ -901,25 +896,52 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
             : "memory");
         wp += 4 * 256;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[g >> 2][4 * (g & 3) + q] = pv[q] + acc[g >> 2][4 * (g & 3) + q];
+        for (int q = 0; q < 4; ++q) {
+          f32x4 &v = acc[g >> 2][4 * (g & 3) + q];
+          v = other_is_start ? pv[q] + v : v + pv[q];
+        }
       }
+    };
+    // first: the piece that starts a tile and is finished by the next workgroup
+    const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
+    if (pubA || pubB) {
+      const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
+      run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 0, 2 * e);
+      publish(slot(t, 0));
+      if (arrive(t)) {  // the end piece came first: this one finishes the tile
+        combine(t, slot(t, 1), false);
+        epilogue(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN);
+        __syncthreads();  // (the epilogue's LDS use before the next piece's K loop)
+      }
+      if (pubA) return;  // (tA's start was the whole range)
+    }
+    // then the piece this workgroup finishes: tA from aA (the end of a split tile), or tA + 1
+    // whole / tA whole
+    const bool finA = !pubA;
+    const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
+    if (!finA && e < nu) return;
+    run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 2 * a, 2 * (e - a));
+    if (a > 0) {  // the end piece of a split tile
+      if (tid == 0) sk_arrived = __hip_atomic_load(sk.cnt + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (sk_arrived == 0) {  // the start piece has not arrived: publish, then count
+        __syncthreads();
+        publish(slot(t, 1));
+        if (!arrive(t)) return;  // the start piece finishes the tile
+      }
+      combine(t, slot(t, 0), true);
     }
     epilogue(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN);
   }
 }
 
-// Stream-K workspace per stream (partials + flags), grown on demand; the epoch tells one
-// launch's flags from the last one's, so the flags are never cleared.
+// Stream-K workspace per stream (two partials per split tile + the arrival counters, which
+// every launch leaves at 0), grown on demand.
 struct SkWs {
   float *ws = nullptr;
-  unsigned *flags = nullptr;
+  unsigned *cnt = nullptr;
   int tiles = 0;
-  unsigned epoch = 0;
 };
-#ifndef VSIM_STREAMK  // (A/B builds: 0 keeps one tile per workgroup)
-#define VSIM_STREAMK 1
-#endif
-constexpr int SK_CUS = 256;
 static int g_streamk = 1;  // vsim_gemm_set_streamk
 int gemm_set_streamk(int on) {
   const int was = g_streamk;
@@ -927,31 +949,58 @@ int gemm_set_streamk(int on) {
   return was;
 }
 
-// the stream's split workspace for `tiles` split tiles (partials, flags, this launch's epoch)
+static std::mutex g_sk_mu;
+static std::map<std::pair<int, hipStream_t>, SkWs> g_sk_ws;  // (device, stream): a null stream is per device
+
+// the stream's split workspace for `tiles` split tiles
 static int sk_workspace(int tiles, hipStream_t s, RSk &sk) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SkWs> per_stream;  // (device, stream): a null stream is per device
   int dev = 0;
   VSIM_HIP(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lock(mu);
-  SkWs &w = per_stream[{dev, s}];
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  SkWs &w = g_sk_ws[{dev, s}];
   if (w.tiles < tiles) {
     if (w.ws) {
       VSIM_HIP(hipStreamSynchronize(s));
       VSIM_HIP(hipFree(w.ws));
-      VSIM_HIP(hipFree(w.flags));
+      VSIM_HIP(hipFree(w.cnt));
     }
-    VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 8 * 32 * 64 * 16));
-    VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)tiles * sizeof(unsigned)));
-    VSIM_HIP(hipMemset(w.flags, 0, (size_t)tiles * sizeof(unsigned)));
+    VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 2 * 8 * 32 * 64 * 16));
+    VSIM_HIP(hipMalloc((void **)&w.cnt, (size_t)tiles * sizeof(unsigned)));
+    VSIM_HIP(hipMemset(w.cnt, 0, (size_t)tiles * sizeof(unsigned)));
     w.tiles = tiles;
-    w.epoch = 0;
   }
-  if (++w.epoch == 0) ++w.epoch;  // (0 is the cleared flag)
   sk.ws = w.ws;
-  sk.flags = w.flags;
-  sk.epoch = w.epoch;
+  sk.cnt = w.cnt;
   return VSIM_OK;
+}
+
+// frees the split workspace of (current device, s) after the stream's work (vsim_model_free)
+int gemm_release_stream(hipStream_t s) {
+  int dev = 0;
+  VSIM_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  auto it = g_sk_ws.find({dev, s});
+  if (it == g_sk_ws.end()) return VSIM_OK;
+  VSIM_HIP(hipStreamSynchronize(s));
+  VSIM_HIP(hipFree(it->second.ws));
+  VSIM_HIP(hipFree(it->second.cnt));
+  g_sk_ws.erase(it);
+  return VSIM_OK;
+}
+
+// CUs of the current device (the stream-K grid is one workgroup per CU)
+static int device_cus() {
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cus.find(dev);
+  if (it != cus.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cus[dev] = n;
+  return n;
 }
 
 // every split tile in at most two pieces (a piece strictly inside a tile would need a third)
@@ -973,9 +1022,9 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
   // (grids of at least half the CUs: each tile in at most two pieces.  GPT-J-6B's 128-tile
   // GEMMs at N = 2048: prompt 32.5 -> 28.5 ms, profiles/r03_streamk_half_grid_ab.jsonl)
   // (the V^T-copy epilogue only below 3/4: at codegen-16B's 192 tiles 167.0 vs 160.9 us with the split)
-  if (VSIM_STREAMK && g_streamk && !GQ && (EM != 3 || nwg * 4 < SK_CUS * 3) && nwg < SK_CUS && nwg * 2 >= SK_CUS &&
-      nu >= 2) {
-    const int upw = (nwg * nu + SK_CUS - 1) / SK_CUS;
+  const int cus = device_cus();
+  if (g_streamk && !GQ && (EM != 3 || nwg * 4 < cus * 3) && nwg < cus && nwg * 2 >= cus && nu >= 2) {
+    const int upw = (nwg * nu + cus - 1) / cus;
     if (sk_two_pieces(nwg, nu, upw)) {
       if (int rc = sk_workspace(nwg, s, sk)) return rc;
       sk.upw = upw;
@@ -1067,9 +1116,10 @@ int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, 
   const int nwg = 2 * (M / R_BM) * ((n + G2_BN - 1) / G2_BN), nu = K / G2_BK / 2;
   RSk sk;
   // hybrid split: the whole rounds as whole tiles, the remainder split over one round of CUs
-  const int wg0 = nwg / SK_CUS * SK_CUS, rest = nwg - wg0;
-  if (VSIM_STREAMK && g_streamk && g_qk_pair == 1 && wg0 > 0 && rest > 0 && nu >= 2) {
-    const int upw = (rest * nu + SK_CUS - 1) / SK_CUS;
+  const int cus = device_cus();
+  const int wg0 = nwg / cus * cus, rest = nwg - wg0;
+  if (g_streamk && g_qk_pair == 1 && wg0 > 0 && rest > 0 && nu >= 2) {
+    const int upw = (rest * nu + cus - 1) / cus;
     if (upw < nu && sk_two_pieces(rest, nu, upw)) {
       if (int rc = sk_workspace(rest, s, sk)) return rc;
       sk.upw = upw;
@@ -1096,9 +1146,6 @@ static int g2_ap(int M, int n) {
     const long tiles = (long)((M + 64 * ap - 1) / (64 * ap)) * ((n + G2_BN - 1) / G2_BN);
     return ((tiles + cus - 1) / cus) * ap;
   };
-#ifdef VSIM_G2_AP  // (A/B builds)
-  return VSIM_G2_AP;
-#endif
   return cost(3) < cost(4) ? 3 : 4;
 }
 
@@ -1141,15 +1188,12 @@ int launch_gemm_q4_256(const W4 &W, const void *x16, int n, const float *bias, f
   return g2_checked(nullptr, &W, W.rows, W.k, x16, n, bias, y, s, q16, epi);
 }
 
-// the register-dequant kernel for every Q4_0 weight with K % 128 == 0 (VSIM_Q4R=0: A/B builds
-// that keep the in-LDS dequant kernel).  Measured at the codegen-16B shapes (N = 2048,
+// the register-dequant kernel for every Q4_0 weight with K % 128 == 0 (the in-LDS dequant
+// kernel for the rest).  Measured at the codegen-16B shapes (N = 2048,
 // tools/gemm_bench.py): 24576 x 6144 941 -> 964-972 TFLOP/s, 6144 x 24576 893-898 -> 916,
 // 6144 x 6144 803 -> 811-824 even though its 192 tiles of 256 rows leave 64 CUs idle (the
 // in-LDS kernel's 256 tiles of 192 rows fill them).
-#ifndef VSIM_Q4R
-#define VSIM_Q4R 1
-#endif
-static bool r_use(int K) { return VSIM_Q4R && K % (2 * G2_BK) == 0; }
+static bool r_use(int K) { return K % (2 * G2_BK) == 0; }
 
 static int g2_checked(const void *A16, const W4 *WQ, int M, int K, const void *x16, int n, const float *bias, float *y,
                       hipStream_t s, void *q16, const G2Epi *epi) {

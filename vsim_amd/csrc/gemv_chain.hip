@@ -219,17 +219,22 @@ __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
 // ================================================================== fused layer tail
 // fc_out, the attention heads and the out-projection of one layer in one launch, so the
 // attention and the out-projection run beside fc_out, whose K = 4E chain is the layer's
-// longest dependency, instead of before it.  Roles by workgroup index:
-//   [0, nf)          fc_out tiles (32-row chain GEMV)
-//   [nf, nf + H)     attention heads (attn.hpp with this kernel's 5 waves); each head
-//                    releases its output and counts itself in *done (agent scope)
-//   [nf + H, ...)    out-projection tiles; wait until *done == H, then acquire
-// Waiting workgroups only wait for lower-indexed ones, which the dispatcher has already
-// placed, so the wait always ends.  *done is zeroed by the layer's LayerNorm kernel.
+// longest dependency, instead of before it.  Roles:
+//   blockIdx [0, nf)   fc_out tiles (32-row chain GEMV)
+//   the rest draw a ticket (an atomic counter, in the order they start running):
+//     ticket [0, na)   attention heads (attn.hpp with this kernel's 5 waves); each head
+//                      releases its output and counts itself in *done (agent scope)
+//     ticket [na, ..)  out-projection tiles; wait until *done == na, then acquire
+// A workgroup holding an out-projection ticket waits only for heads whose tickets were drawn
+// before its own, i.e. by workgroups already running: the wait ends whatever order or placement
+// the dispatcher picks.  The wait is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it
+// the error counter (vsim_spin_timeouts) is bumped and the tile goes on.  *done and *ticket
+// are zeroed by the layer's LayerNorm kernel.
+constexpr unsigned TAIL_SPIN_MAX = 1u << 22;
 struct TailJob {
   GemvBatch f, o;
   AttnJob a;
-  unsigned *done;
+  unsigned *done, *ticket, *err;
   int nf;
 };
 
@@ -238,12 +243,15 @@ __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
     C2Lds g;
     float a[sizeof(C2Lds) / sizeof(float)];
   } L;
+  __shared__ unsigned role;
   int b = blockIdx.x;
   if (b < T.nf) {
     chain32_body(T.f, b, L.g);
     return;
   }
-  b -= T.nf;
+  if (threadIdx.x == 0) role = __hip_atomic_fetch_add(T.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  b = (int)role;
   const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
   if (b < na) {
     attn_body<C2_THREADS>(T.a, b, L.a);
@@ -253,9 +261,16 @@ __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
     return;
   }
   b -= na;
-  if (threadIdx.x == 0)
-    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)na)
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)na) {
       __builtin_amdgcn_s_sleep(8);
+      if (++spins == TAIL_SPIN_MAX) {
+        if (T.err) __hip_atomic_fetch_add(T.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   chain32_body(T.o, b, L.g);
@@ -274,12 +289,14 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   T.o = o;
   T.a = a;
   T.done = done;
+  T.ticket = done + 64;  // (a separate 256-byte line; zeroed with *done by the LayerNorm kernel)
+  T.err = spin_error_counter();
   T.nf = 0;
   for (int i = 0; i < f.nj; ++i) T.nf += f.j[i].w.tiles;
   int no = 0;
   for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;
   // dynamic LDS pad: above half the CU's LDS, so one workgroup per CU (fc_out's consumer
-  // keeps its SIMD); the out-projection tiles that find no CU start as attention heads end
+  // keeps its SIMD); the workgroups that find no CU start as attention heads end
   hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H * S + no), dim3(C2_THREADS), 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
@@ -374,7 +391,6 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
       __builtin_amdgcn_sched_barrier(0);
       ldx(k + 1, xn);
       __builtin_amdgcn_sched_barrier(0);
-#ifndef VSIM_SOLO_NOPROD  // (A/B experiment builds: loads and barriers only)
       {
         const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
         const float dl = 512.0f * dv, ml = -8.0f * dv;
@@ -390,7 +406,6 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
           *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
         }
       }
-#endif
       ps = ps == C5_RING - 1 ? 0 : ps + 1;
       __builtin_amdgcn_sched_barrier(0);
       producer_barrier();
@@ -431,14 +446,10 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
 #pragma unroll
       for (int j = 0; j < S::CP / 4; ++j) {
         const float4 v = win[j % S::WIN];
-#ifdef VSIM_SOLO_NOCHAIN  // (A/B experiment builds: the reads without the dependent adds)
-        acc = fmaxf(acc, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
-#else
         acc = acc + v.x;
         acc = acc + v.y;
         acc = acc + v.z;
         acc = acc + v.w;
-#endif
         const int jn = j + S::WIN;
         win[j % S::WIN] = jn < S::CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - S::CP / 4));
         __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
@@ -486,14 +497,8 @@ static int solo_groups(const GemvBatch &B, int cons = 1) {
 // them to cover the CUs, else 32-row workgroups (k_gemv_chain32: more CUs per row, for
 // fc_out and the out-projection, whose K = 4E chains are the whole cost).
 constexpr int SOLO_CB = 6, SOLO_PF = 3, SOLO_MIN_GROUPS = 192;
-#ifndef VSIM_SOLO_CONS2  // (A/B experiment builds: 0 keeps every batch on the 64-row groups)
-#define VSIM_SOLO_CONS2 0
-#endif
 
 bool gemv_chain_solo(const GemvBatch &B) { return solo_groups(B) >= SOLO_MIN_GROUPS; }
-// 128-row groups when they still cover most CUs (the Q, K, V + fc_in batch: 224 groups in one
-// round instead of 448 at two per CU)
-static bool solo_cons2(const GemvBatch &B) { return VSIM_SOLO_CONS2 && solo_groups(B, 2) >= SOLO_MIN_GROUPS; }
 
 int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
   int tiles = 0;
@@ -506,15 +511,9 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     tiles += B.j[i].w.tiles;
   }
   if (tiles == 0) return VSIM_OK;
-  if (solo_cons2(B)) {
-    hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 2>), dim3(solo_groups(B, 2)),
-                       dim3(64 * SoloShape<SOLO_CB, 2>::WAVES), 0, s, B);
-  } else if (gemv_chain_solo(B)) {
-#ifndef VSIM_SOLO_LDS_PAD  // (A/B experiment builds: dynamic LDS that limits workgroups per CU)
-#define VSIM_SOLO_LDS_PAD 0
-#endif
+  if (gemv_chain_solo(B)) {
     hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)), dim3(64 * SoloShape<SOLO_CB, 1>::WAVES),
-                       VSIM_SOLO_LDS_PAD, s, B);
+                       0, s, B);
   } else {
     hipLaunchKernelGGL(k_gemv_chain32, dim3(tiles), dim3(C2_THREADS), 0, s, B);
   }

@@ -28,16 +28,12 @@ extern unsigned *g_norm_stats;
 // ------------------------------------------------------------------ 1. LN + quantize
 // One 1024-thread workgroup per LayerNorm (two for GPT-NeoX's parallel-residual pair); the
 // normalized row is quantized by whole waves, two 32-blocks per wave step.
-#ifndef VSIM_LNQ_THREADS  // (A/B builds: tools/variant.sh)
-#define VSIM_LNQ_THREADS 512
-#define VSIM_LNQ_SPLIT 8
-#endif
-constexpr int LNQ_THREADS = VSIM_LNQ_THREADS;
+constexpr int LNQ_THREADS = 512;
 
 // LNQ_SPLIT workgroups per LayerNorm: each computes the whole row's statistics (the row is
 // 16 KB, read from L2) and normalizes, writes and quantizes one slice of LNQ_SPLIT, so the
 // latency-bound per-element phases run on LNQ_SPLIT CUs.
-constexpr int LNQ_SPLIT = VSIM_LNQ_SPLIT;
+constexpr int LNQ_SPLIT = 8;
 __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuantJob j1, int n, unsigned *stats) {
   extern __shared__ __attribute__((aligned(16))) float row[];
   const int part = blockIdx.x % LNQ_SPLIT;

@@ -551,9 +551,9 @@ int run_layer_bloom(vsim_model *m, int il, int n_past, int N, int &nk) {
   RC(launch_rope_kv_write(0, m->Qb, m->Kb, m->Vb, kc, vc, d, H, N, n_past, 0, m->rope_cs, s)); ++nk;  // no rotary
   const int nkv = n_past + N;
   const float scale = (float)(1.0f / std::sqrt((double)(float(E) / H)));
-  RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
+  RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s, n_past)); ++nk;
   RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s, m->alibi)); ++nk;
-  RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
+  RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s, n_past)); ++nk;
   RC(act16(m->attn_in, E, xb, nullptr, false));
   RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, L.bo, m->attn, nk, xb));
   // inpFF = attn + inpL (kept in cur2), its LayerNorm into cur1
@@ -659,9 +659,9 @@ int run_layer(vsim_model *m, int il, int n_past, int N, int &nk) {
                                kv16_epi, attn_q16 ? X.b : nullptr));
     nk += 2;
   } else {
-    RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s)); ++nk;
+    RC(launch_kq(kc, E, m->Qb, E, d, H, nkv, N, m->kq, s, n_past)); ++nk;
     RC(launch_attn_softmax(m->kq, nkv, N, H, n_past, scale, s)); ++nk;
-    RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s)); ++nk;
+    RC(launch_kqv(vc, E, m->kq, d, H, nkv, N, m->attn_in, 1, s, n_past)); ++nk;
   }
   if (!attn_q16) RC(act16(m->attn_in, E, X.b, nullptr, false));
   RC(mm(m, L.wo, E, E, m->attn_in, N, m->xq2, m->xd2, true, gptj ? nullptr : L.bo, m->attn, nk, X.b));
@@ -1269,6 +1269,7 @@ void vsim_model_free(vsim_model *m) {
   if (m->kcache && !m->borrowed) (void)hipFree(m->kcache);
   if (m->vcache && !m->borrowed) (void)hipFree(m->vcache);
   if (m->rope_cs) (void)hipFree(m->rope_cs);
+  if (m->stream) (void)gemm_release_stream(m->stream);  // the prompt GEMM's stream-K workspace
   if (m->stream) (void)hipStreamDestroy(m->stream);
   for (hipEvent_t e : m->prof_events) (void)hipEventDestroy(e);
   delete m;

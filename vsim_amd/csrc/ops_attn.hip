@@ -122,33 +122,7 @@ int launch_rope_kv_write(int style, float *Q, const float *K, const float *V, fl
   return VSIM_OK;
 }
 
-// KQ[h][q][k] = (float) sum_i (double)(K[k][h*d+i] * Q[q][h*d+i]), sequential in i.
-__global__ void k_kq(const float *__restrict__ K, int ldk, const float *__restrict__ Q, int ldq, int d, int H, int nk,
-                     int n, float *__restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= H * n * nk) return;
-  const int k = i % nk, q = (i / nk) % n, h = i / (nk * n);
-  const float *kr = K + (size_t)k * ldk + h * d;
-  const float *qr = Q + (size_t)q * ldq + h * d;
-  double s = 0.0;
-  for (int j = 0; j < d; j += 4) {
-    const float4 a = *(const float4 *)(kr + j);
-    const float4 b = *(const float4 *)(qr + j);
-    s += (double)(a.x * b.x);
-    s += (double)(a.y * b.y);
-    s += (double)(a.z * b.z);
-    s += (double)(a.w * b.w);
-  }
-  out[i] = (float)s;
-}
-
-int launch_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq, hipStream_t s) {
-  if (d % 4 || ldk % 4 || ldq % 4) { set_error("kq: d and strides must be multiples of 4"); return VSIM_EINVAL; }
-  const int tot = H * n * nk;
-  hipLaunchKernelGGL(k_kq, dim3((tot + 255) / 256), dim3(256), 0, s, K, ldk, Q, ldq, d, H, nk, n, kq);
-  VSIM_HIP(hipGetLastError());
-  return VSIM_OK;
-}
+// (KQ and KQV: attn_exact.hip)
 
 // scale -> mask -> softmax, one 256-thread block per row of nc (row r = (z, j)).
 // The fp16-valued exps sum exactly in double in any order (multiples of 2^-24, < 2^11).
@@ -199,32 +173,6 @@ int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scal
   DevTables t;
   if (int rc = tables_get(&t)) return rc;
   hipLaunchKernelGGL(k_attn_softmax, dim3(nr * nz), dim3(256), 0, s, p, nc, nr, n_past, scale, t.exp_f16, alibi);
-  VSIM_HIP(hipGetLastError());
-  return VSIM_OK;
-}
-
-// out = sum_k V[k][h*d+dd] * S[h][q][k], sequential float chain in k starting at 0.
-// merged = 0: out[(h*n + q)*d + dd] (the reference's KQV [d, N, H] tensor)
-// merged = 1: out[q*E + h*d + dd]    (after KQV_merged + cpy, vsim.cpp:610-616)
-__global__ void k_kqv(const float *__restrict__ V, int ldv, const float *__restrict__ S, int d, int H, int nk, int n,
-                      float *__restrict__ out, int merged) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= H * n * d) return;
-  const int dd = i % d, q = (i / d) % n, h = i / (d * n);
-  const float *srow = S + ((size_t)h * n + q) * nk;
-  const float *vcol = V + h * d + dd;
-  float y = 0.0f;
-  for (int k = 0; k < nk; ++k) y = y + vcol[(size_t)k * ldv] * srow[k];
-  if (merged)
-    out[(size_t)q * H * d + h * d + dd] = y;
-  else
-    out[i] = y;
-}
-
-int launch_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, int merged,
-               hipStream_t s) {
-  const int tot = H * n * d;
-  hipLaunchKernelGGL(k_kqv, dim3((tot + 255) / 256), dim3(256), 0, s, V, ldv, S, d, H, nk, n, out, merged);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

@@ -218,6 +218,15 @@ int tables_host(uint16_t *exp_f16, uint16_t *gelu_f16) {
   return VSIM_OK;
 }
 
+// g_norm_stats[2]: bounded cross-workgroup waits that gave up (k_layer_tail); 0 in a healthy run
+unsigned *spin_error_counter() { return g_norm_stats ? g_norm_stats + 2 : nullptr; }
+int spin_timeouts(unsigned *out) {
+  *out = 0;
+  if (!g_norm_stats) return VSIM_OK;
+  VSIM_HIP(hipMemcpy(out, g_norm_stats + 2, sizeof(unsigned), hipMemcpyDeviceToHost));
+  return VSIM_OK;
+}
+
 int norm_stats(unsigned *out2) {
   if (!g_norm_stats) { out2[0] = out2[1] = 0; return VSIM_OK; }
   unsigned h[4];

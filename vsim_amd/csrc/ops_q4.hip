@@ -157,37 +157,6 @@ int launch_q4_dequant(const void *xq, int rows, int k, float *y, hipStream_t s) 
   return VSIM_OK;
 }
 
-// ------------------------------------------------------------------ exact GEMV (N tokens)
-// One lane per (row, token) chain, reference order.  Used for prompt batches (N > 1).
-__global__ void __launch_bounds__(256) k_gemv_exact_rows(W4 W, const float *__restrict__ xd, int n,
-                                                          const float *__restrict__ bias, float *__restrict__ y) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ic = blockIdx.y;
-  if (r >= W.rows || ic >= n) return;
-  const int nb = W.nb();
-  const float *xr = xd + (size_t)ic * W.k;
-  float acc = 0.0f;
-  for (int i = 0; i < nb; ++i) {
-    const size_t o = W.off(r, i);
-    const float d0 = W.d[o];
-    const uint4 q = *(const uint4 *)(W.qs + o * 16);
-    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int wv = 0; wv < 4; ++wv) {
-      const float4 a = *(const float4 *)(xr + i * QK + wv * 8);
-      const float4 b = *(const float4 *)(xr + i * QK + wv * 8 + 4);
-      const float x8[8] = {a.x, a.z, a.y, a.w, b.x, b.z, b.y, b.w};  // pair-interleaved (xd_slot)
-      float p4[4];
-      pair_terms4(qw[wv], d0, x8, p4);
-      acc = acc + p4[0];
-      acc = acc + p4[1];
-      acc = acc + p4[2];
-      acc = acc + p4[3];
-    }
-  }
-  y[(size_t)ic * W.rows + r] = bias ? acc + bias[r] : acc;
-}
-
 // ------------------------------------------------------------------ activation quantize
 // (quantize_block: kern.hpp)
 
@@ -253,11 +222,8 @@ int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd,
   if (mode == VSIM_MODE_EXACT && !xd) { set_error("q4_gemv: exact mode needs xd"); return VSIM_EINVAL; }
   // fast mode, prompt batches: fp16 MFMA GEMM after in-LDS dequant (gemm_f16.hip)
   if (mode == VSIM_MODE_FAST && n >= GEMM_MIN_N) return launch_gemm_q4_f16(W, xq, n, bias, y, s);
-  if (mode == VSIM_MODE_EXACT && n > 1) {
-    hipLaunchKernelGGL(k_gemv_exact_rows, dim3((M + 255) / 256, n), dim3(256), 0, s, W, xd, n, bias, y);
-    VSIM_HIP(hipGetLastError());
-    return VSIM_OK;
-  }
+  // exact mode, prompt batches: the register-tiled chain GEMM (gemm_exact.hip)
+  if (mode == VSIM_MODE_EXACT && n > 1) return launch_gemm_exact(W, xd, n, bias, y, s);
   const size_t nbk = (size_t)n * (K / QK);
   const uint8_t *xqs = (const uint8_t *)xq;
   const float *xdd = (const float *)(xqs + nbk * 16);

@@ -26,7 +26,7 @@ EXPORTS = [
     "vsim_last_error", "vsim_device_count", "vsim_q4_bytes",
     "init_xmax", "imax_ggml_compute_forward_mul_mat_q4_0_f32",
     "vsim_ggml_gptneox_rope_f32", "vsim_ggml_rope_f32", "vsim_ggml_soft_max_f32", "vsim_ggml_mul_mat_f32",
-    "vsim_dropin_stats", "vsim_dropin_reset", "vsim_norm_fallbacks",
+    "vsim_dropin_stats", "vsim_dropin_reset", "vsim_norm_fallbacks", "vsim_spin_timeouts",
     "vsim_op_q4_repack", "vsim_op_q4_unpack", "vsim_op_act_repack", "vsim_op_act_unpack",
     "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_q4_expand_f16", "vsim_op_gemm_f16",
     "vsim_op_act_quant_f16", "vsim_op_gemm_f16_gelu_q", "vsim_op_gemm_f16_rope", "vsim_op_gemm_f16_join",
@@ -324,6 +324,13 @@ def norm_fallbacks():
     out = (ctypes.c_uint * 2)()
     check(lib().vsim_norm_fallbacks(out), "norm_fallbacks")
     return int(out[0]), int(out[1])
+
+
+def spin_timeouts():
+    """Bounded cross-workgroup waits that gave up so far (0 in a healthy run)."""
+    out = ctypes.c_uint()
+    check(lib().vsim_spin_timeouts(ctypes.byref(out)), "spin_timeouts")
+    return int(out.value)
 
 
 def dropin_stats():
