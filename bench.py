@@ -17,8 +17,8 @@ default run also measures that split over the same N ranks in a child job and re
 beside the headline as `pipeline_20b` (north star: 1/2/4/8-GPU numbers for the 20B).
 
 Prints ONE JSON line (rank 0) with `roofline` (the Q4_0 GEMV kernel: algorithmic weight
-bytes / event-timed average launch) and `cpu_baseline` (the CPU oracle on the host cores,
-1 GPT-J layer + lm_head sample extrapolated to 28 layers).
+bytes / event-timed average launch) and `cpu_baseline` (the CPU oracle on the host cores: the
+full 28-layer model, decode tokens timed at the job's threads and at 1 thread).
 """
 from __future__ import annotations
 
@@ -160,33 +160,32 @@ def host_cpu():
     return os.cpu_count() or 1, model, max(1, avail)
 
 
-def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12, n_tokens_1t: int = 4):
-    """CPU oracle (port of the reference path) on a bounded sample, tokens/s extrapolated, at
-    every thread of this job's CPU share and at 1 thread."""
+def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 4, n_tokens_1t: int = 2):
+    """CPU oracle (port of the reference path) on the host cores: the full-depth model of the
+    config (every layer, synthetic weights of its shapes), a 1-token prompt, then `n_tokens`
+    decode tokens timed at every thread of this job's CPU share and `n_tokens_1t` at 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     arch = {"gptneox": 0, "gptj": 1, "bloom": 2}[arch_s]  # VO_ARCH_*
     nproc, model_name, nth = host_cpu()
+    t0 = time.perf_counter()
+    m = O.Model(None, arch, n_ctx=1 + n_tokens + n_tokens_1t + 1,
+                synthetic=(hp.n_vocab, hp.n_embd, hp.n_head, hp.n_layer, hp.n_rot, 7, 0.02))
+    t_make = time.perf_counter() - t0
+    m.eval(0, PROMPT[:1], nthreads=nth)
+    n_past = 1
 
-    def per_token(n_layer, threads, n):
-        m = O.Model(None, arch, n_ctx=5 + n + 1,
-                    synthetic=(hp.n_vocab, hp.n_embd, hp.n_head, n_layer, hp.n_rot, 7, 0.02))
-        m.eval(0, PROMPT, nthreads=threads)
-        t0 = time.perf_counter()
+    def per_token(threads, n):
+        nonlocal n_past
+        t = time.perf_counter()
         for i in range(n):
-            m.eval(5 + i, [i + 11], nthreads=threads)
-        dt = (time.perf_counter() - t0) / n
-        del m
-        return dt
+            m.eval(n_past, [i + 11], nthreads=threads)
+            n_past += 1
+        return (time.perf_counter() - t) / n
 
-    def tok_time(threads, n):
-        t1 = per_token(1, threads, n)
-        t0 = per_token(0, threads, n)
-        t_layer = max(t1 - t0, 1e-9)
-        return hp.n_layer * t_layer + t0, t_layer, t0
-
-    t_all, tl_all, t0_all = tok_time(nth, n_tokens)
-    t_one, tl_one, t0_one = tok_time(1, n_tokens_1t)
+    t_all = per_token(nth, n_tokens)
+    t_one = per_token(1, n_tokens_1t)
+    del m
     speed = None
     sp = sorted(glob_profiles("*_oracle_vs_ref_speed.json"))
     if sp:
@@ -199,12 +198,10 @@ def cpu_baseline(arch_s: str, hp: mg.HParams, n_tokens: int = 12, n_tokens_1t: i
         "kind": "port",
         "value_1_thread": round(1.0 / t_one, 4),
         "host": {"nproc": nproc, "model_name": model_name, "threads_available_to_job": nth},
-        "sample": (f"oracle/vsim_oracle.cpp (scalar restatement of imax.c:1182-1230 et al.); decode tokens "
-                   f"on a 1-layer and a 0-layer model of {arch_s} width (E={hp.n_embd}, V={hp.n_vocab}), "
-                   f"per-token = {hp.n_layer}*(t1-t0)+t0. {nth} threads ({n_tokens} tokens): "
-                   f"{t_all * 1e3:.1f} ms (t_layer {tl_all * 1e3:.1f}, t_embed+head {t0_all * 1e3:.1f}); "
-                   f"1 thread ({n_tokens_1t} tokens): {t_one * 1e3:.1f} ms (t_layer {tl_one * 1e3:.1f}, "
-                   f"t_embed+head {t0_one * 1e3:.1f})"),
+        "sample": (f"oracle/vsim_oracle.cpp (scalar restatement of imax.c:1182-1230 et al.), the full "
+                   f"{hp.n_layer}-layer {arch_s} model (E={hp.n_embd}, V={hp.n_vocab}, synthetic weights, "
+                   f"{t_make:.1f} s to make), 1-token prompt, then {n_tokens} decode tokens timed at {nth} "
+                   f"threads: {t_all * 1e3:.1f} ms each; {n_tokens_1t} more at 1 thread: {t_one * 1e3:.1f} ms each"),
         "oracle_vs_reference_speed": ({"file": os.path.relpath(sp[-1], ROOT), "threads": speed.get("threads")}
                                       if speed else None),
     }
@@ -262,7 +259,7 @@ def run_pipeline(args, world, rank, dev, dist):
     arch_s, hp = mg.CONFIGS[args.config]
     arch = ARCHS[arch_s]
     L = hp.n_layer
-    per = (L + world - 1) // world
+    per = pipeline.layer_split(L, world)
     l0, l1 = pipeline.layer_range(L, world, rank)
     n_ctx = max(512, len(PROMPT) + args.warmup + args.steps + 16)
     hpd = dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head, n_layer=L, n_rot=hp.n_rot,

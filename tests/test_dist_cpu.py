@@ -15,14 +15,14 @@ from vsim_amd import pipeline
 E, V, L = 16, 11, 7
 
 
-def _weights():
+def _weights(nl=L):
     rng = np.random.default_rng(3)
-    return (rng.standard_normal((V, E)).astype(np.float32), rng.standard_normal((L, E, E)).astype(np.float32) * 0.3,
+    return (rng.standard_normal((V, E)).astype(np.float32), rng.standard_normal((nl, E, E)).astype(np.float32) * 0.3,
             rng.standard_normal((V, E)).astype(np.float32))
 
 
-def _stage_fn(l0, l1, first, last, kv):
-    emb, layers, head = _weights()
+def _stage_fn(l0, l1, first, last, kv, nl=L):
+    emb, layers, head = _weights(nl)
 
     def stage(n_past, ids, resid_in, resid_out):
         x = emb[np.asarray(ids)] if first else resid_in.numpy().copy()
@@ -82,12 +82,19 @@ def _stream(world):
 
 
 def test_layer_ranges_tile_the_model():
-    for world in (1, 2, 3, 4, 7):
-        spans = [pipeline.layer_range(L, world, r) for r in range(world)]
-        assert spans[0][0] == 0 and spans[-1][1] == L
-        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    for nl in (L, 28, 36, 44):
+        for world in (w for w in (1, 2, 3, 4, 7, 8) if w <= nl):
+            spans = [pipeline.layer_range(nl, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == nl
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = pipeline.layer_split(nl, world)
+            assert max(sizes) - min(sizes) <= 1 and min(sizes) >= 1
+    # the 20B's splits of SURVEY.md §8(e)
+    assert pipeline.layer_split(44, 2) == [22, 22]
+    assert pipeline.layer_split(44, 4) == [11] * 4
+    assert pipeline.layer_split(44, 8) == [6, 6, 6, 6, 5, 5, 5, 5]
     with pytest.raises(ValueError):
-        pipeline.layer_range(L, 8, 7)  # 8 ranks for 7 layers: the last rank would be empty
+        pipeline.layer_range(L, 8, 7)  # 8 ranks for 7 layers: a rank would be empty
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -95,7 +102,7 @@ def test_pipeline_matches_single_rank(world):
     assert _stream(world) == _stream(1)
 
 
-def _run_steps(rank, world, port, out, host_staged=False):
+def _run_steps(rank, world, port, out, host_staged=False, nl=L):
     """pipeline.decode_steps with a stand-in stage step over bound buffers (the device-resident
     protocol of vsim_model_stage_step: token word in on rank 0, residual rows between ranks,
     argmax token word out on the last rank), after a pipeline_step prompt.  The hand-offs are
@@ -105,9 +112,9 @@ def _run_steps(rank, world, port, out, host_staged=False):
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     first, last = rank == 0, rank == world - 1
-    l0, l1 = pipeline.layer_range(L, world, rank)
+    l0, l1 = pipeline.layer_range(nl, world, rank)
     kv = {}
-    stage = _stage_fn(l0, l1, first, last, kv)
+    stage = _stage_fn(l0, l1, first, last, kv, nl)
     syncs = []
     send, recv = pipeline.make_transport(dist, host_staged, sync=lambda: syncs.append(1)) if world > 1 else (None, None)
     prompt = [1, 4, 2]
@@ -157,6 +164,27 @@ def test_decode_steps_match_single_rank(world, host_staged):
     assert stream(world) == stream(1) == _stream(1)
 
 
+def test_decode_steps_world8_20b_split():
+    """World 8 over gloo at the 20B's depth (44 layers as 6,6,6,6,5,5,5,5):
+    the stream-ordered (RCCL-branch) transport's send/recv sequence through eight stand-in
+    stages gives the single rank's token stream."""
+    ctx = mp.get_context("spawn")
+
+    def stream(w):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_run_steps, args=(r, w, port, q, False, 44)) for r in range(w)]
+        for p in procs:
+            p.start()
+        toks = q.get(timeout=180)
+        for p in procs:
+            p.join(timeout=180)
+            assert p.exitcode == 0
+        return toks
+
+    assert stream(8) == stream(1)
+
+
 def test_bench_pipeline_companion_env_and_failure(monkeypatch):
     """bench.py's `pipeline_20b` companion: the child job gets a rendezvous of its own (no
     TORCHELASTIC_* agent store, MASTER_PORT + 17, the parent's rank) and a child that fails
@@ -191,6 +219,11 @@ def test_bench_pipeline_companion_env_and_failure(monkeypatch):
     assert "--pipeline" in seen["cmd"] and "gpt-neoxt-20b" in seen["cmd"] and seen["kw"]["timeout"] > 0
     # rank 1 returns nothing; a failing or hanging child is an error entry
     assert bench.pipeline_companion(args, world=2, rank=1, local=1) is None
+    # the driver's 8-GPU run: rank 7 of 8 starts its child as rank 7 of an 8-rank job, bounded
+    assert bench.pipeline_companion(args, world=8, rank=7, local=7) is None
+    env = seen["env"]
+    assert env["RANK"] == "7" and env["WORLD_SIZE"] == "8" and env["LOCAL_RANK"] == "7"
+    assert 0 < seen["kw"]["timeout"] <= 600
     R.returncode = 3
     assert bench.pipeline_companion(args, world=2, rank=0, local=0)["error"] == "exit 3"
 

@@ -5,8 +5,9 @@ models bench.py times, with bench.py's weights (vsim_model_randomize, seed 1234,
   * GPT-J-6B, all 28 layers: the 5-token prompt, then 24 greedy decode steps, logits as bits
     at every step; then the device greedy loop (the bench's timed step) over the same steps;
   * pythia-12b (36 layers) and GPT-NeoXT-20B (44 layers): prompt + 8 decode steps;
-  * GPT-NeoXT-20B as a 4-stage layer split in one process (11 layers per stage, the residual
-    handed over in device memory): the last stage's logits equal the oracle's.
+  * GPT-NeoXT-20B as a 4- and an 8-stage layer split in one process (11 x 4 and 6,6,6,6,5,5,5,5
+    layers, the residual handed over in device memory): the last stage's
+    logits equal the oracle's.
 The per-layer KV offsets il*n_ctx (vsim.cpp:555-556) and the layer loop (vsim.cpp:521-701)
 are exercised at every depth; n_ctx is kept small (64) to bound the oracle's cache.
 The oracle's rows are independent chains, so its thread count does not change any bit.
@@ -98,18 +99,18 @@ def _copy_stage(full, st, arch_s, hp):
         hip.check(hip.lib().vsim_model_set_tensor(st.h, name.encode(), buf.ctypes.data, nbytes), name)
 
 
-def test_20b_four_stage_split_full_depth_bit_exact():
-    """GPT-NeoXT-20B, 44 layers as 4 stages of 11 (the 4-GPU split of bench.py --pipeline,
-    here on one device): prompt + 8 decode steps through the chain of stages, the last stage's
-    logits equal the oracle's whole-model logits at every step."""
+@pytest.mark.parametrize("G,split", [(4, [11, 11, 11, 11]), (8, [6, 6, 6, 6, 5, 5, 5, 5])])
+def test_20b_stage_split_full_depth_bit_exact(G, split):
+    """GPT-NeoXT-20B, 44 layers as G stages (the 4- and 8-GPU splits of bench.py --pipeline,
+    pipeline.layer_range, here on one device): prompt + 8 decode steps through the chain of
+    stages, the last stage's logits equal the oracle's whole-model logits at every step."""
     import torch
+    from vsim_amd import pipeline
     arch_s, hp, dm, om = _bench_pair("gpt-neoxt-20b")
     _, _, hpd = _hp("gpt-neoxt-20b")
-    G = 4
-    per = -(-hp.n_layer // G)
-    stages = [hip.Model.create(hip.ARCH_GPTNEOX, hpd, n_ctx=N_CTX, layer_begin=g * per,
-                               layer_end=min(hp.n_layer, (g + 1) * per)) for g in range(G)]
-    assert [s.layer_end - s.layer_begin for s in stages] == [11, 11, 11, 11]
+    spans = [pipeline.layer_range(hp.n_layer, G, g) for g in range(G)]
+    stages = [hip.Model.create(hip.ARCH_GPTNEOX, hpd, n_ctx=N_CTX, layer_begin=a, layer_end=b) for a, b in spans]
+    assert [s.layer_end - s.layer_begin for s in stages] == split
     for st in stages:
         _copy_stage(dm, st, arch_s, hp)
         st.set_graph(True)

@@ -195,6 +195,43 @@ def test_stage_step_needs_fresh_begin_after_eval(tmp_path):
     m.close()
 
 
+def test_kernel_counts_per_graph_kind(tmp_path):
+    """kernels_per_eval after each call reports that call's own step, whichever of the four
+    decode graphs (eval, eval_argmax, generate, stage step) was captured last: with the graph
+    on, captured in a mixed order, each equals the count of the same call with the graph off."""
+    import torch
+    arch_s, hp = mg.CONFIGS["tiny-neox"]
+    path = str(tmp_path / "kc.bin")
+    mg.write_model(path, arch_s, hp, seed=4, std=0.05)
+    m = hip.Model.load(path, hip.ARCH_GPTNEOX, n_ctx=64)
+    tok = torch.zeros(1, dtype=torch.int32, device="cuda")
+    m.stage_bind(tok_in=tok.data_ptr(), tok_out=tok.data_ptr())
+    m.eval(0, [1, 2, 3])
+
+    def counts(graph):
+        m.set_graph(graph)
+        out = {}
+        m.generate(3, 4, 1)
+        out["generate"] = m.info()["kernels_per_eval"]
+        m.stage_begin(4)
+        m.stage_step()
+        out["stage"] = m.info()["kernels_per_eval"]
+        m.eval_argmax(5, 6)
+        out["argmax"] = m.info()["kernels_per_eval"]
+        m.eval(6, [7])
+        out["eval"] = m.info()["kernels_per_eval"]
+        m.stage_begin(7)
+        m.stage_step()
+        out["stage2"] = m.info()["kernels_per_eval"]
+        return out
+
+    off, on = counts(False), counts(True)
+    assert on == off, (on, off)
+    assert off["argmax"] == off["eval"] + 1 and off["stage"] == off["stage2"]
+    m.sync()
+    m.close()
+
+
 @pytest.mark.parametrize("cfg", ["small-gptj", "small-neox", "small-bloom", "small-neox-serial"])
 def test_graph_replay_bit_exact_vs_oracle(cfg, tmp_path):
     """The decode step captured once in a hipGraph and replayed (n_past and the token read

@@ -33,7 +33,7 @@ def free_port():
                                                      ("small-neox", 2, 0, None)])
 def test_pipeline_ranks_equal_single_stage(cfg, world, graph, n_layer, tmp_path):
     arch_s, hp = mg.CONFIGS[cfg]
-    if n_layer:  # more layers than ranks, uneven splits (ceil(5/3) = 2, 2, 1; ceil(7/4) = 2, 2, 2, 1)
+    if n_layer:  # more layers than ranks, uneven splits (pipeline.layer_range: 5/3 = 2, 2, 1; 7/4 = 2, 2, 2, 1)
         hp = mg.HParams(hp.n_vocab, hp.n_embd, hp.n_head, n_layer, hp.n_rot, hp.use_parallel_residual)
     arch = hip.ARCH_GPTJ if arch_s == "gptj" else hip.ARCH_GPTNEOX
     path = str(tmp_path / f"{cfg}.bin")

@@ -27,9 +27,11 @@ NTH = max(1, min(16, os.cpu_count() or 1))
 # distribution profiles/r03_fast_prefill_e2e_distribution.json (tools/fast_prefill_distribution.py:
 # 72 prompts of these three models at N = 72 and 288, other prompts than the ones below):
 # cos min 0.9741, 5th percentile 0.9771, median 0.9884; the fast greedy token within the oracle's
-# top 5 in 72 of 72, equal to the oracle's in 49 of 72 (so no per-prompt top-1 bound).  The
-# cos bound is the recorded minimum less a margin of 0.014; neither is edited after a red run.
-FAST_COS_MIN = 0.96
+# top 5 in 72 of 72, equal to the oracle's in 49 of 72 (68 %: no per-prompt top-1 bound, but at
+# least 2 of each model's 4 prompts at N = 72).  The cos bound is the recorded minimum less a
+# margin of 0.004 (r04: back from r03's 0.96); neither is edited after a red run.
+FAST_COS_MIN = 0.97
+FAST_TOP1_MIN_N72 = 2  # of 4 prompts
 
 
 def bits(a):
@@ -87,6 +89,8 @@ def test_fast_prompt_vs_oracle(cfg, N, tmp_path):
     msg = f"{cfg}: cos {['%.5f' % c for c in cos]}, max-rel {['%.3g' % r[1] for r in res]}, top-1 {top1}/4"
     print(msg)
     assert min(cos) >= FAST_COS_MIN, msg
+    if N == 72:
+        assert top1 >= FAST_TOP1_MIN_N72, msg
     # the greedy token: the random parity models' top logits are close and the re-quantization
     # flips of fast mode move them past each other (top-1 49/72 recorded), so the bound is the
     # oracle's top 5 (72/72 recorded)

@@ -50,7 +50,7 @@ __device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::
 // scalar loads.
 constexpr int C2_CB = 8, C2_CP = C2_CB * 16, C2_LD = C2_CP + 4, C2_NPW = C2_CB / 2;
 constexpr int C2_THREADS = 64 * (1 + C2_NPW);
-constexpr int C2_RING = 3, C2_WIN = 8, C2_DEPTH = 4, C2_RAW = C2_DEPTH;  // raw slot reuse: see below
+constexpr int C2_RING = 3, C2_WIN = 16, C2_DEPTH = 4, C2_RAW = C2_DEPTH;  // raw slot reuse: see below
 constexpr int C2_WAIT_VM3 = 0x0F70 | (3 * (C2_DEPTH - 2));  // wave 1: nibbles, scales, factors
 constexpr int C2_WAIT_VM2 = 0x0F70 | (2 * (C2_DEPTH - 2));  // other producers: nibbles, scales
 static_assert(3 * (C2_DEPTH - 2) < 16, "vmcnt immediate");
@@ -219,22 +219,25 @@ __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
 // ================================================================== fused layer tail
 // fc_out, the attention heads and the out-projection of one layer in one launch, so the
 // attention and the out-projection run beside fc_out, whose K = 4E chain is the layer's
-// longest dependency, instead of before it.  Roles:
-//   blockIdx [0, nf)   fc_out tiles (32-row chain GEMV)
-//   the rest draw a ticket (an atomic counter, in the order they start running):
-//     ticket [0, na)   attention heads (attn.hpp with this kernel's 5 waves); each head
-//                      releases its output and counts itself in *done (agent scope)
-//     ticket [na, ..)  out-projection tiles; wait until *done == na, then acquire
-// A workgroup holding an out-projection ticket waits only for heads whose tickets were drawn
-// before its own, i.e. by workgroups already running: the wait ends whatever order or placement
-// the dispatcher picks.  The wait is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it
-// the error counter (vsim_spin_timeouts) is bumped and the tile goes on.  *done and *ticket
-// are zeroed by the layer's LayerNorm kernel.
+// longest dependency, instead of before it.  Roles by workgroup index:
+//   [0, nf)          fc_out tiles (32-row chain GEMV)
+//   [nf, nf + na)    attention heads (attn.hpp with this kernel's 5 waves); each head
+//                    releases its output and counts itself in *done (agent scope)
+//   [nf + na, ...)   out-projection tiles; wait until *done == na, then acquire
+// Waiting workgroups only wait for lower-indexed ones, which the dispatcher places first on
+// this part (and fc_out's tiles never wait, so the CUs they hold always come free); the wait
+// is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it the error counter
+// (vsim_spin_timeouts) is bumped and the tile goes on.  r04 measured two placement-independent
+// role assignments (tools/tail_ab.sh): every role by a start-order ticket, 55.8 vs 40.9 us per
+// tail; heads pulled from a claim counter by the head workgroups and, when unclaimed, by the
+// out-projection tiles before they wait: a bloom-560m full-width decode differed from the
+// oracle at a late step (not understood; the variant without stealing passed).  Neither is
+// kept.  *done is zeroed by the layer's LayerNorm kernel.
 constexpr unsigned TAIL_SPIN_MAX = 1u << 22;
 struct TailJob {
   GemvBatch f, o;
   AttnJob a;
-  unsigned *done, *ticket, *err;
+  unsigned *done, *err;
   int nf;
 };
 
@@ -243,15 +246,12 @@ __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
     C2Lds g;
     float a[sizeof(C2Lds) / sizeof(float)];
   } L;
-  __shared__ unsigned role;
   int b = blockIdx.x;
   if (b < T.nf) {
     chain32_body(T.f, b, L.g);
     return;
   }
-  if (threadIdx.x == 0) role = __hip_atomic_fetch_add(T.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  b = (int)role;
+  b -= T.nf;
   const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
   if (b < na) {
     attn_body<C2_THREADS>(T.a, b, L.a);
@@ -289,7 +289,6 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   T.o = o;
   T.a = a;
   T.done = done;
-  T.ticket = done + 64;  // (a separate 256-byte line; zeroed with *done by the LayerNorm kernel)
   T.err = spin_error_counter();
   T.nf = 0;
   for (int i = 0; i < f.nj; ++i) T.nf += f.j[i].w.tiles;
@@ -323,7 +322,7 @@ struct SoloShape {
   // the rest only join the barriers; the others are the producers
   static constexpr int WAVES = PRODUCERS + (PRODUCERS + 2) / 3;  // a 0-mod-4 slot per 3 producers
   static constexpr int ROWS = 64 * CONS;
-  static constexpr int WIN = CP / 4 % 8 == 0 ? 8 : 12;
+  static constexpr int WIN = 12;  // (r04: 12 and chain32's 16 read deeper than r03's 8: tail -1.1 us)
   static_assert(CP / 4 % WIN == 0, "the read window must tile the chunk");
   static_assert(WAVES <= 16, "workgroup size");
   static_assert((WAVES + 3) / 4 >= CONS, "consumer waves on one SIMD");

@@ -611,13 +611,20 @@ bool match_neox_decode(const ggml_cgraph *g, NeoxMatch &M, std::string &why) {
   return true;
 }
 
-// what a plan is bound to: every matched weight and the cache, the thread count, the scale
+// what a plan is bound to: every matched weight and the cache - each tensor struct and its
+// data pointer, so a tensor whose struct stays put while its data moves takes a new plan (and
+// the per-node path's re-registration) instead of the stale mirrors
 std::vector<const void *> plan_key(const NeoxMatch &M) {
-  std::vector<const void *> k{M.wte, M.lmh, M.lnf_w, M.lnf_b, M.memk, M.memv};
+  std::vector<const void *> k;
+  auto add = [&](const ggml_tensor *t) {
+    k.push_back(t);
+    k.push_back(t ? t->data : nullptr);
+  };
+  for (const ggml_tensor *t : {M.wte, M.lmh, M.lnf_w, M.lnf_b, M.memk, M.memv}) add(t);
   for (const NeoxLayer &Y : M.layers)
     for (const ggml_tensor *t : {Y.ln1_w, Y.ln1_b, Y.ln2_w, Y.ln2_b, Y.wq, Y.bq, Y.wk, Y.bk, Y.wv, Y.bv, Y.wo, Y.bo,
                                  Y.wfc, Y.bfc, Y.wproj, Y.bproj})
-      k.push_back(t);
+      add(t);
   return k;
 }
 

@@ -116,7 +116,6 @@ struct vsim_model {
   size_t pf_bytes = 0;
 
   int graph_mode = -1;
-  int graph_kernels = 0;
   // graph executor's fast path (graph.cpp): weights and KV cache borrowed from its device
   // mirrors (not freed here), the KQV key grouping of the caller's thread count and the
   // scale the graph carries (0: computed from the hparams)
@@ -1581,7 +1580,6 @@ int decode_graph(vsim_model *m, int kind) {
   graph = g;
   VSIM_HIP(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
   gmode = m->mode;
-  m->graph_kernels = gk;
   m->graph_kernels_kind[kind] = gk;
   return VSIM_OK;
 }
@@ -1687,7 +1685,7 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
       // when the graph runs)
       RC(decode_graph(m, 0));
       VSIM_HIP(hipGraphLaunch(m->gexec, s));
-      nk = m->graph_kernels;
+      nk = m->graph_kernels_kind[0];
     } else {
       RC(upload_step(m));
       RC(enqueue_decode(m, nk));
@@ -1782,7 +1780,7 @@ int vsim_model_stage_step(vsim_model *m) {
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 3));
     VSIM_HIP(hipGraphLaunch(m->gexec_st, m->stream));
-    m->kernels_last = m->graph_kernels_kind[1];
+    m->kernels_last = m->graph_kernels_kind[3];
   } else {
     int nk = 0;
     RC(enqueue_stage(m, nk));

@@ -23,12 +23,18 @@ import numpy as np
 
 
 def layer_range(n_layer: int, world: int, rank: int) -> tuple[int, int]:
-    """Contiguous split, ceil(L/G) layers per rank (the last ranks may hold fewer)."""
-    per = (n_layer + world - 1) // world
-    l0, l1 = min(n_layer, rank * per), min(n_layer, (rank + 1) * per)
-    if l1 <= l0:
-        raise ValueError(f"{world} ranks for {n_layer} layers leaves rank {rank} without layers")
-    return l0, l1
+    """Contiguous balanced split: the first L % G ranks hold ceil(L/G) layers, the rest
+    floor(L/G) (the 20B's 44 layers as 22/22, 11 x 4, 6,6,6,6,5,5,5,5)."""
+    if world > n_layer:
+        raise ValueError(f"{world} ranks for {n_layer} layers leaves a rank without layers")
+    base, extra = divmod(n_layer, world)
+    l0 = rank * base + min(rank, extra)
+    return l0, l0 + base + (1 if rank < extra else 0)
+
+
+def layer_split(n_layer: int, world: int) -> list[int]:
+    """Layers per rank of layer_range."""
+    return [b - a for a, b in (layer_range(n_layer, world, r) for r in range(world))]
 
 
 def make_transport(dist, host_staged: bool, sync: Callable | None = None):
