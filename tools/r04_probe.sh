@@ -22,6 +22,10 @@ if [ "${1:-}" = suite ]; then
     > "$out/r04_race.log" 2>&1
   rc3=$?; echo "[probe] race screen exit=$rc3"; tail -3 "$out/r04_race.log"
   if [ "$rc3" -ne 0 ]; then exit "$rc3"; fi
+  for i in 1 2; do
+    timeout -k 10 300 python3 "$root/bench.py" --config codegen-16B --prefill 2048 --steps 3 > "$out/r04_pf_$i.log" 2>&1 || exit 4
+    echo "[probe] prefill $(grep -o '"ms_per_prompt": [0-9.]*' "$out/r04_pf_$i.log" | head -1)"
+  done
   timeout -k 10 300 python3 "$root/bench.py" --no-cpu-baseline --no-pipeline-20b > "$out/r04_bench.log" 2>&1
   rc3=$?; echo "[probe] bench exit=$rc3"; tail -1 "$out/r04_bench.log" | cut -c1-300
   if [ "$rc3" -ne 0 ]; then exit "$rc3"; fi

@@ -673,24 +673,30 @@ constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
 // Stream-K (sk.upw > 0, for grids of fewer tiles than CUs: the 192 tiles of every 6144-row
 // codegen-16B GEMM): the grid is one workgroup per CU and workgroup b takes the K-tile pairs
 // ("units") [b upw, (b + 1) upw) of the tiles laid end to end, so every CU does the same work.
-// A tile split between two workgroups has a start piece (K from 0) and an end piece.  Nobody
-// waits for anybody (no assumption on dispatch order or co-residence): each piece counts its
-// arrival on the tile's counter (agent-scope atomic), and whichever arrives second adds the
-// other's partial (partial_start + partial_end, one rounded add per value: the same bits
-// whichever piece finishes) and runs the epilogue, then clears the counter for the next launch.
-//  * the start piece (computed first) always publishes its partial (write-through sc1 stores in
-//    the register layout, drained) before it counts;
-//  * the end piece (computed last) first looks at the counter: when the start has arrived (the
-//    usual case) it finishes without publishing; otherwise it publishes its own partial, counts,
-//    and finishes only if the start arrived in between.
+// A tile split between two workgroups: the one holding its start (the lower index) computes that
+// part first thing and publishes its accumulators (write-through sc1 stores in the register
+// layout, drained, then an sc1 flag holding this launch's epoch); the one holding its end
+// computes that part last, polls the flag (sc1), adds the partial with sc1 loads (one rounded
+// add per value: partial + own, the same in every run) and runs the epilogue.  The launcher
+// checks no tile has 3 pieces and sizes the grid to the device's CUs (at most one workgroup per
+// CU is needed for all of them to be resident at once).  The publisher publishes before it waits
+// on anything, so whatever order the workgroups are dispatched in, a waiter's publisher runs as
+// soon as it has a CU; the wait is bounded all the same (SK_SPIN_MAX sleeps, ~1 s: past it the
+// error counter vsim_spin_timeouts is bumped).  r04 tried a wait-free variant (the second of
+// the two pieces to arrive finishes the tile, from an atomic counter): with two epilogue sites
+// the kernel spilled 100-350 VGPRs (scratch traffic beside the counted vmcnt waits) and ran
+// 0.5 ms slower per codegen-16B prompt (61.7 vs 61.1-61.2 ms); not kept.
 // Hybrid split (PAIR launches, wg0 > 0): workgroups [0, wg0) take the whole tiles [0, wg0) (a
 // full round of the CUs), the rest run the split above over the tiles from t0 = wg0 on.
 struct RSk {
-  int upw = 0;           // units (K-tile pairs) per workgroup; 0: one tile per workgroup
-  float *ws = nullptr;   // partials: [tile - t0][piece: 0 start, 1 end][wave][32 f32x4][64 lanes]
-  unsigned *cnt = nullptr;  // arrivals per split tile (0 between launches)
+  int upw = 0;          // units (K-tile pairs) per workgroup; 0: one tile per workgroup
+  float *ws = nullptr;  // partials: [tile - t0][wave][32 f32x4][64 lanes]
+  unsigned *flags = nullptr;
+  unsigned epoch = 0;
+  unsigned *err = nullptr;  // bounded-wait timeouts (vsim_spin_timeouts)
   int wg0 = 0, t0 = 0;
 };
+constexpr unsigned SK_SPIN_MAX = 1u << 23;
 
 // PAIR: two GEMMs of the same shape (M rows each: the Q and K projections of a long GPT-J
 // prompt, both with the RoPE epilogue) in one launch.  The tile grid covers 2M rows; tiles of
@@ -853,9 +859,12 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     const int u0 = ((int)blockIdx.x - (PAIR ? sk.wg0 : 0)) * sk.upw, u1 = min(u0 + sk.upw, (nwg - t0) * nu);
     const int tA = u0 / nu, aA = u0 - tA * nu, eA = min(u1 - tA * nu, nu);
     const int eB = max(u1 - (tA + 1) * nu, 0);  // units of tA + 1 from its start
-    __shared__ unsigned sk_arrived;
-    auto slot = [&](int t, int piece) { return sk.ws + ((size_t)((2 * t + piece) * 8 + wave) * 32 * 64 + lane) * 4; };
-    auto publish = [&](float *wp) __attribute__((always_inline)) {
+    // first: the piece that starts a tile and is finished by the next workgroup (published)
+    const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
+    if (pubA || pubB) {
+      const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
+      run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 0, 2 * e);
+      float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
       // (4 stores per base address, offsets 0-3 KB)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -872,16 +881,28 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-    };
-    // this piece's arrival on tile t's counter; true when it is the second (it finishes)
-    auto arrive = [&](int t) __attribute__((always_inline)) -> bool {
-      if (tid == 0) sk_arrived = __hip_atomic_fetch_add(sk.cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(sk.flags + t, sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pubA) return;  // (tA's start was the whole range)
+    }
+    // then the piece this workgroup finishes: tA from aA (after a published tA + 1 start), or
+    // tA + 1 whole / tA whole
+    const bool finA = !pubA;
+    const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
+    if (!finA && e < nu) return;
+    run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 2 * a, 2 * (e - a));
+    if (a > 0) {  // the earlier part's partial
+      if (tid == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(sk.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sk.epoch) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins == SK_SPIN_MAX) {
+            if (sk.err) __hip_atomic_fetch_add(sk.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
       __syncthreads();
-      return sk_arrived != 0;
-    };
-    // acc = partial_start + partial_end, `other` the piece not in acc; the counter cleared
-    auto combine = [&](int t, const float *wp, bool other_is_start) __attribute__((always_inline)) {
-      if (tid == 0) __hip_atomic_store(sk.cnt + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
 #pragma unroll
       for (int g = 0; g < 8; ++g) {  // 4 registers' worth at a time (acc holds 128 VGPRs)
         f32x4 pv[4];
@@ -896,51 +917,20 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
             : "memory");
         wp += 4 * 256;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f32x4 &v = acc[g >> 2][4 * (g & 3) + q];
-          v = other_is_start ? pv[q] + v : v + pv[q];
-        }
+        for (int q = 0; q < 4; ++q) acc[g >> 2][4 * (g & 3) + q] = pv[q] + acc[g >> 2][4 * (g & 3) + q];
       }
-    };
-    // first: the piece that starts a tile and is finished by the next workgroup
-    const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
-    if (pubA || pubB) {
-      const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
-      run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 0, 2 * e);
-      publish(slot(t, 0));
-      if (arrive(t)) {  // the end piece came first: this one finishes the tile
-        combine(t, slot(t, 1), false);
-        epilogue(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN);
-        __syncthreads();  // (the epilogue's LDS use before the next piece's K loop)
-      }
-      if (pubA) return;  // (tA's start was the whole range)
-    }
-    // then the piece this workgroup finishes: tA from aA (the end of a split tile), or tA + 1
-    // whole / tA whole
-    const bool finA = !pubA;
-    const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
-    if (!finA && e < nu) return;
-    run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 2 * a, 2 * (e - a));
-    if (a > 0) {  // the end piece of a split tile
-      if (tid == 0) sk_arrived = __hip_atomic_load(sk.cnt + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      if (sk_arrived == 0) {  // the start piece has not arrived: publish, then count
-        __syncthreads();
-        publish(slot(t, 1));
-        if (!arrive(t)) return;  // the start piece finishes the tile
-      }
-      combine(t, slot(t, 0), true);
     }
     epilogue(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN);
   }
 }
 
-// Stream-K workspace per stream (two partials per split tile + the arrival counters, which
-// every launch leaves at 0), grown on demand.
+// Stream-K workspace per stream (partials + flags), grown on demand; the epoch tells one
+// launch's flags from the last one's, so the flags are never cleared.
 struct SkWs {
   float *ws = nullptr;
-  unsigned *cnt = nullptr;
+  unsigned *flags = nullptr;
   int tiles = 0;
+  unsigned epoch = 0;
 };
 static int g_streamk = 1;  // vsim_gemm_set_streamk
 int gemm_set_streamk(int on) {
@@ -952,7 +942,7 @@ int gemm_set_streamk(int on) {
 static std::mutex g_sk_mu;
 static std::map<std::pair<int, hipStream_t>, SkWs> g_sk_ws;  // (device, stream): a null stream is per device
 
-// the stream's split workspace for `tiles` split tiles
+// the stream's split workspace for `tiles` split tiles (partials, flags, this launch's epoch)
 static int sk_workspace(int tiles, hipStream_t s, RSk &sk) {
   int dev = 0;
   VSIM_HIP(hipGetDevice(&dev));
@@ -962,15 +952,19 @@ static int sk_workspace(int tiles, hipStream_t s, RSk &sk) {
     if (w.ws) {
       VSIM_HIP(hipStreamSynchronize(s));
       VSIM_HIP(hipFree(w.ws));
-      VSIM_HIP(hipFree(w.cnt));
+      VSIM_HIP(hipFree(w.flags));
     }
-    VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 2 * 8 * 32 * 64 * 16));
-    VSIM_HIP(hipMalloc((void **)&w.cnt, (size_t)tiles * sizeof(unsigned)));
-    VSIM_HIP(hipMemset(w.cnt, 0, (size_t)tiles * sizeof(unsigned)));
+    VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 8 * 32 * 64 * 16));
+    VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)tiles * sizeof(unsigned)));
+    VSIM_HIP(hipMemset(w.flags, 0, (size_t)tiles * sizeof(unsigned)));
     w.tiles = tiles;
+    w.epoch = 0;
   }
+  if (++w.epoch == 0) ++w.epoch;  // (0 is the cleared flag)
   sk.ws = w.ws;
-  sk.cnt = w.cnt;
+  sk.flags = w.flags;
+  sk.epoch = w.epoch;
+  sk.err = spin_error_counter();
   return VSIM_OK;
 }
 
@@ -983,7 +977,7 @@ int gemm_release_stream(hipStream_t s) {
   if (it == g_sk_ws.end()) return VSIM_OK;
   VSIM_HIP(hipStreamSynchronize(s));
   VSIM_HIP(hipFree(it->second.ws));
-  VSIM_HIP(hipFree(it->second.cnt));
+  VSIM_HIP(hipFree(it->second.flags));
   g_sk_ws.erase(it);
   return VSIM_OK;
 }
