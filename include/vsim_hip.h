@@ -241,6 +241,11 @@ int vsim_model_get_tensor(vsim_model *m, const char *name, void *host, size_t nb
  * quantize_row_q4_0 semantics; for throughput runs of full-size configs. */
 int vsim_model_randomize(vsim_model *m, uint64_t seed, float std);
 int vsim_model_set_mode(vsim_model *m, int mode);
+/* Allocates ahead what a prompt of up to n_tokens sets up on its first eval (the N-token
+ * scratch, the fp16 key copies of the prompt attention, the GEMMs' stream-K workspace) and
+ * loads the prompt kernels, so that the first prompt runs at the steady-state rate.  Optional:
+ * an eval allocates whatever is missing itself.  VSIM_EINVAL if n_tokens is not in 1..n_ctx. */
+int vsim_model_reserve(vsim_model *m, int n_tokens);
 int vsim_model_hparams(const vsim_model *m, vsim_hparams *hp, int *n_ctx, int *layer_begin, int *layer_end);
 /* One eval of N tokens at n_past (vsim.cpp:470-747).  First stage reads `tokens`;
  * non-first stages read the residual from `resid_in` (device, [N][n_embd] f32);

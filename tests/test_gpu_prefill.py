@@ -167,3 +167,26 @@ def test_gptj_width_prefill_n2048():
     assert np.array_equal(bits(lf), bits(lf2)), "fast prompt not deterministic"
     assert cos >= FAST_COS_MIN, msg
     dm.close()
+
+
+def test_reserve_ahead_of_prompt():
+    """vsim_model_reserve allocates a prompt's buffers and stream-K workspace ahead of the first
+    eval: the prompt after it gives the same bits as on a model that allocates them on the way
+    (fast mode, GPT-J-6B width, N = 2048: the paired Q/K launch with its hybrid split and the
+    half-grid split of V), and out-of-range sizes are refused."""
+    N = 2048
+    ids = [(7919 * i + 11) % GPTJ6B["n_vocab"] for i in range(N)]
+    out = []
+    for reserve in (True, False):
+        dm = hip.Model.create(hip.ARCH_GPTJ, GPTJ6B, n_ctx=N + 8)
+        dm.randomize(seed=31, std=0.02)
+        dm.set_mode(hip.MODE_FAST)
+        if reserve:
+            for bad in (0, N + 9):
+                with pytest.raises(hip.VsimError):
+                    dm.reserve(bad)
+            dm.reserve(N)
+        out.append(dm.eval(0, ids))
+        dm.close()
+    assert not np.isnan(out[0]).any()
+    assert np.array_equal(bits(out[0]), bits(out[1]))

@@ -18,6 +18,8 @@
 //    MFMA operand that sums over the accumulator's row index needs no lane movement
 //    (cdna_hip_programming.md §3); V is staged transposed in LDS with the matching k
 //    order.  O^T (head dim x 32 queries) lives in the accumulator registers.
+#include <mutex>
+
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
@@ -549,12 +551,7 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
   const float qscale = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
   const dim3 grid(((N + AP_BQ - 1) / AP_BQ) * H);
   if (d == 256) {
-    static bool attr2 = false;
-    if (!attr2) {
-      VSIM_HIP(hipFuncSetAttribute((const void *)k_attn_prefill_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)ap2_lds()));
-      attr2 = true;
-    }
+    if (int rc = attn_prefill_prepare()) return rc;
     hipLaunchKernelGGL(k_attn_prefill_pair, grid, dim3(AP2_THREADS), ap2_lds(), s, Q, k16, vt16, E, H, N, n_past, ldt,
                        qscale, out, (_Float16 *)out16);
     VSIM_HIP(hipGetLastError());
@@ -573,6 +570,26 @@ int launch_attn_prefill_f16(const float *Q, const float *kc, const float *vc, in
   VSIM_HIP(hipGetLastError());
   if (own) VSIM_HIP(hipFreeAsync(buf, s));
   return VSIM_OK;
+}
+
+// the pair kernel's LDS attribute, once per process; the other instances' attributes are read
+// so that their code object is loaded before a timed prompt (vsim_model_reserve)
+int attn_prefill_prepare() {
+  static std::once_flag once;
+  static int rc = VSIM_OK;
+  std::call_once(once, [] {
+    hipFuncAttributes fa;
+    if (hipFuncSetAttribute((const void *)k_attn_prefill_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)ap2_lds()) != hipSuccess ||
+        hipFuncGetAttributes(&fa, (const void *)k_attn_prefill_f16<64>) != hipSuccess ||
+        hipFuncGetAttributes(&fa, (const void *)k_attn_prefill_f16<96>) != hipSuccess ||
+        hipFuncGetAttributes(&fa, (const void *)k_attn_prefill_f16<128>) != hipSuccess ||
+        hipFuncGetAttributes(&fa, (const void *)k_kv_f16) != hipSuccess) {
+      set_error("attention prefill: kernel attributes refused");
+      rc = VSIM_EHIP;
+    }
+  });
+  return rc;
 }
 
 size_t attn_prefill_scratch(int E, int nk) {

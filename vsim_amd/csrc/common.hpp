@@ -317,8 +317,10 @@ int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, 
                             const G2Epi &e1, hipStream_t s);
 bool gemm_pair_enabled(int M, int K);
 int gemm_set_qk_pair(int mode);  // vsim_gemm_set_qk_pair (0 off, 1 default, 2 no split); returns the old setting
-int gemm_set_streamk(int on);
-int gemm_release_stream(hipStream_t s);  // frees the stream-K workspace of (current device, s)  // stream-K split of the register-dequant GEMM (default on); returns the old setting
+int gemm_set_streamk(int on);  // stream-K split of the register-dequant GEMM (default on); returns the old setting
+int gemm_release_stream(hipStream_t s);  // frees the stream-K workspace of (current device, s)
+int gemm_reserve_stream(hipStream_t s);  // the split workspace and kernel attributes, ahead of a prompt
+int attn_prefill_prepare();              // the prompt attention's kernel attributes
 bool attn_prefill_supported(int d);
 // scratch: attn_prefill_scratch(E, n_past + N) bytes for the fp16 K / V^T copies (null or
 // smaller: allocated stream-ordered per call); fresh: the new keys [n_past, n_past + N) are

@@ -942,30 +942,54 @@ int gemm_set_streamk(int on) {
 static std::mutex g_sk_mu;
 static std::map<std::pair<int, hipStream_t>, SkWs> g_sk_ws;  // (device, stream): a null stream is per device
 
+static int device_cus();
+
+// (a split never covers a full round of CUs: sized for one, the workspace is allocated once per
+// stream and a prompt's later, larger split does not synchronize the stream to grow it)
+static int sk_grow(SkWs &w, int tiles, hipStream_t s) {
+  tiles = std::max(tiles, device_cus());
+  if (w.tiles >= tiles) return VSIM_OK;
+  if (w.ws) {
+    VSIM_HIP(hipStreamSynchronize(s));
+    VSIM_HIP(hipFree(w.ws));
+    VSIM_HIP(hipFree(w.flags));
+  }
+  VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 8 * 32 * 64 * 16));
+  VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)tiles * sizeof(unsigned)));
+  VSIM_HIP(hipMemset(w.flags, 0, (size_t)tiles * sizeof(unsigned)));
+  w.tiles = tiles;
+  w.epoch = 0;
+  return VSIM_OK;
+}
+
 // the stream's split workspace for `tiles` split tiles (partials, flags, this launch's epoch)
 static int sk_workspace(int tiles, hipStream_t s, RSk &sk) {
   int dev = 0;
   VSIM_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lock(g_sk_mu);
   SkWs &w = g_sk_ws[{dev, s}];
-  if (w.tiles < tiles) {
-    if (w.ws) {
-      VSIM_HIP(hipStreamSynchronize(s));
-      VSIM_HIP(hipFree(w.ws));
-      VSIM_HIP(hipFree(w.flags));
-    }
-    VSIM_HIP(hipMalloc((void **)&w.ws, (size_t)tiles * 8 * 32 * 64 * 16));
-    VSIM_HIP(hipMalloc((void **)&w.flags, (size_t)tiles * sizeof(unsigned)));
-    VSIM_HIP(hipMemset(w.flags, 0, (size_t)tiles * sizeof(unsigned)));
-    w.tiles = tiles;
-    w.epoch = 0;
-  }
+  if (int rc = sk_grow(w, tiles, s)) return rc;
   if (++w.epoch == 0) ++w.epoch;  // (0 is the cleared flag)
   sk.ws = w.ws;
   sk.flags = w.flags;
   sk.epoch = w.epoch;
   sk.err = spin_error_counter();
   return VSIM_OK;
+}
+
+static int r_attrs();
+
+// everything a long prompt's GEMMs set up on first use, done ahead (vsim_model_reserve): the
+// split workspace of (current device, s) and the kernels' LDS attributes (which also loads
+// their code object)
+int gemm_reserve_stream(hipStream_t s) {
+  int dev = 0;
+  VSIM_HIP(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> lock(g_sk_mu);
+    if (int rc = sk_grow(g_sk_ws[{dev, s}], 0, s)) return rc;
+  }
+  return r_attrs();
 }
 
 // frees the split workspace of (current device, s) after the stream's work (vsim_model_free)
@@ -1027,12 +1051,6 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
   }
   if constexpr (!GQ) {
     if (sk.upw) {
-      static bool attr = false;
-      if (!attr) {
-        VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_q4r<GQ, EM, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     r_lds_bytes()));
-        attr = true;
-      }
       hipLaunchKernelGGL((k_gemm_q4r<GQ, EM, true>), dim3(grid), dim3(G2_THREADS), r_lds_bytes(), s, WQ, M, K,
                          (const _Float16 *)x16, n, bias, y, tab, (_Float16 *)q16, epi, sk, RPair{});
       return VSIM_OK;
@@ -1043,17 +1061,29 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
   return VSIM_OK;
 }
 
+// the LDS attribute of every k_gemm_q4r instance, once per process
+static int r_attrs() {
+  static std::once_flag once;
+  static int rc = VSIM_OK;
+  std::call_once(once, [] {
+    const void *fns[] = {(const void *)k_gemm_q4r<false, 0>,          (const void *)k_gemm_q4r<false, 1>,
+                         (const void *)k_gemm_q4r<false, 2>,          (const void *)k_gemm_q4r<false, 3>,
+                         (const void *)k_gemm_q4r<true, 0>,           (const void *)k_gemm_q4r<false, 0, true>,
+                         (const void *)k_gemm_q4r<false, 1, true>,    (const void *)k_gemm_q4r<false, 2, true>,
+                         (const void *)k_gemm_q4r<false, 3, true>,    (const void *)k_gemm_q4r<false, 1, false, true>,
+                         (const void *)k_gemm_q4r<false, 1, true, true>};
+    for (const void *f : fns)
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()) != hipSuccess) {
+        set_error("k_gemm_q4r: LDS attribute refused");
+        rc = VSIM_EHIP;
+      }
+  });
+  return rc;
+}
+
 static int r_launch(const W4 &WQ, int M, int K, const void *x16, int n, const float *bias, float *y, hipStream_t s,
                     const uint16_t *tab, void *q16, const G2Epi &epi) {
-  static bool attr = false;
-  if (!attr) {
-    const void *fns[] = {(const void *)k_gemm_q4r<false, 0>, (const void *)k_gemm_q4r<false, 1>,
-                         (const void *)k_gemm_q4r<false, 2>, (const void *)k_gemm_q4r<false, 3>,
-                         (const void *)k_gemm_q4r<true, 0>};
-    for (const void *f : fns)
-      VSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
-    attr = true;
-  }
+  if (int rc = r_attrs()) return rc;
   int rc;
   if (q16) rc = r_go<true, 0>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
   else if (epi.cs) rc = r_go<false, 1>(WQ, M, K, x16, n, bias, y, tab, q16, epi, s);
@@ -1095,14 +1125,7 @@ int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, 
     set_error("gemm pair: two M x K weights (M % 256 == 0, K % 128 == 0) with RoPE epilogues of one head shape");
     return VSIM_EINVAL;
   }
-  static bool attr = false;
-  if (!attr) {
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_q4r<false, 1, false, true>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
-    VSIM_HIP(hipFuncSetAttribute((const void *)k_gemm_q4r<false, 1, true, true>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, r_lds_bytes()));
-    attr = true;
-  }
+  if (int rc = r_attrs()) return rc;
   RPair pr;
   pr.w = W1;
   pr.y = y1;

@@ -1658,6 +1658,24 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   return VSIM_OK;
 }
 
+int vsim_model_reserve(vsim_model *m, int n_tokens) {
+  if (!m) { set_error("reserve: null model"); return VSIM_EINVAL; }
+  if (n_tokens <= 0 || n_tokens > m->n_ctx) { set_error("reserve: n_tokens must be in 1..n_ctx"); return VSIM_EINVAL; }
+  VSIM_HIP(hipSetDevice(m->device));
+  RC(ensure_scratch(m, n_tokens));
+  const int E = E_(m), d = E / m->hp.n_head;
+  if (n_tokens >= 8 && attn_prefill_supported(d) && E % 64 == 0) {
+    if (!m->pf_scratch) {
+      m->pf_bytes = attn_prefill_scratch(E, m->n_ctx);
+      VSIM_HIP(hipMalloc(&m->pf_scratch, m->pf_bytes));
+    }
+    RC(attn_prefill_prepare());
+  }
+  if (n_tokens >= G2_MIN_N) RC(gemm_reserve_stream(m->stream));
+  VSIM_HIP(hipStreamSynchronize(m->stream));
+  return VSIM_OK;
+}
+
 int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, const float *resid_in, float *resid_out,
                     float *logits) {
   if (!m) { set_error("eval: null model"); return VSIM_EINVAL; }

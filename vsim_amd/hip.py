@@ -36,7 +36,7 @@ EXPORTS = [
     "vsim_op_tables",
     "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_get_tensor",
     "vsim_model_randomize",
-    "vsim_model_set_mode", "vsim_model_hparams", "vsim_model_eval", "vsim_model_eval_argmax", "vsim_model_generate",
+    "vsim_model_set_mode", "vsim_model_reserve", "vsim_model_hparams", "vsim_model_eval", "vsim_model_eval_argmax", "vsim_model_generate",
     "vsim_model_stream",
     "vsim_model_logits_dev", "vsim_model_info", "vsim_model_set_graph", "vsim_model_set_profile",
     "vsim_model_profile_kernel", "vsim_model_profile_stats", "vsim_model_free",
@@ -140,6 +140,7 @@ def lib():
     L.vsim_model_get_tensor.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.vsim_model_randomize.argtypes = [vp, ctypes.c_uint64, cf]
     L.vsim_model_set_mode.argtypes = [vp, ci]
+    L.vsim_model_reserve.argtypes = [vp, ci]
     L.vsim_model_set_graph.argtypes = [vp, ci]
     L.vsim_model_hparams.argtypes = [vp, ctypes.POINTER(HParams), ctypes.POINTER(ci), ctypes.POINTER(ci),
                                      ctypes.POINTER(ci)]
@@ -238,6 +239,10 @@ class Model:
 
     def set_mode(self, mode):
         check(lib().vsim_model_set_mode(self.h, mode), "set_mode")
+
+    def reserve(self, n_tokens):
+        """Allocates a prompt of up to n_tokens' buffers and loads its kernels ahead of the first eval."""
+        check(lib().vsim_model_reserve(self.h, n_tokens), "reserve")
 
     def set_graph(self, enable: bool):
         check(lib().vsim_model_set_graph(self.h, 1 if enable else 0), "set_graph")

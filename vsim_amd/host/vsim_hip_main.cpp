@@ -221,6 +221,11 @@ int run(const Params &params, int arch) {
 
   std::vector<float> logits(hp.n_vocab);
   const int32_t warm[5] = {1, 2, 3, 4, 5};
+  if (!embd_inp.empty() && (int)embd_inp.size() <= n_ctx &&
+      vsim_model_reserve(model, (int)embd_inp.size()) != VSIM_OK) {
+    fprintf(stderr, "reserve failed: %s\n", vsim_last_error());
+    return 1;
+  }
   if (vsim_model_eval(model, 0, warm, 5, nullptr, nullptr, logits.data()) != VSIM_OK) {
     fprintf(stderr, "warm-up eval failed: %s\n", vsim_last_error());
     return 1;
