@@ -51,9 +51,11 @@ __device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::
 constexpr int C2_CB = 8, C2_CP = C2_CB * 16, C2_LD = C2_CP + 4, C2_NPW = C2_CB / 2;
 constexpr int C2_THREADS = 64 * (1 + C2_NPW);
 constexpr int C2_RING = 3, C2_WIN = 16, C2_DEPTH = 4, C2_RAW = C2_DEPTH;  // raw slot reuse: see below
-constexpr int C2_WAIT_VM3 = 0x0F70 | (3 * (C2_DEPTH - 2));  // wave 1: nibbles, scales, factors
-constexpr int C2_WAIT_VM2 = 0x0F70 | (2 * (C2_DEPTH - 2));  // other producers: nibbles, scales
-static_assert(3 * (C2_DEPTH - 2) < 16, "vmcnt immediate");
+// s_waitcnt vmcnt(n) alone (expcnt, lgkmcnt at their maxima): n's low 4 bits in [3:0], high 2 in [15:14]
+constexpr int waitcnt_vm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+constexpr int C2_WAIT_VM3 = waitcnt_vm(3 * (C2_DEPTH - 2));  // wave 1: nibbles, scales, factors
+constexpr int C2_WAIT_VM2 = waitcnt_vm(2 * (C2_DEPTH - 2));  // other producers: nibbles, scales
+static_assert(3 * (C2_DEPTH - 2) < 64, "vmcnt immediate");
 
 struct C2Lds {
   float P[C2_RING][32 * C2_LD];

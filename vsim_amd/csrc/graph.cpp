@@ -869,6 +869,7 @@ void vsim_graph_reset(void) {
     if (kv.second.w4) (void)hipFree(kv.second.w4);
   }
   X.ext.clear();
+  if (X.stream && hipSetDevice(X.device) == hipSuccess) (void)gemm_release_stream(X.stream);  // stream-K workspace
   if (X.arena_dev) (void)hipFree(X.arena_dev);
   X.arena_dev = nullptr;
   X.arena_host = nullptr;
