@@ -211,6 +211,12 @@ int vsim_op_gemm_q4_256_pair(const void *w0, const void *w1, int M, int K, const
  * paired launch, its remainder past whole rounds of the CUs split as above; 2: paired, whole
  * tiles only.  Process-wide; returns the previous setting. */
 int vsim_gemm_set_qk_pair(int mode);
+/* Order of the long-prompt GEMM's 256 x 256 tiles over the grid: groups of `cols` tile-columns
+ * (256 tokens each), each group walked row by row, so the tiles one XCD runs together share
+ * fewer activation slices; 0 = one group (row-major).  Used only when it divides the tile
+ * columns.  Outputs do not depend on the order, except that a stream-K split then falls at other
+ * tiles (same per-element bound).  Process-wide; returns the previous setting. */
+int vsim_gemm_set_tile_order(int cols);
 /* Fast-mode prompt LayerNorm (ggml_norm + affine, ggml.c:4246-4304, double sums in any order)
  * straight to the next GEMM's fp16 operand: quantize_row_q4_0 per 32-value block, d*(q-8) as
  * fp16 -- what vsim_op_act_quant_f16 makes of the normalized rows. */

@@ -156,6 +156,7 @@ int vsim_op_attn_prefill_q16(const float *Q, const float *kc, const float *vc, i
 int vsim_op_tables(uint16_t *exp_f16_host, uint16_t *gelu_f16_host) { return tables_host(exp_f16_host, gelu_f16_host); }
 int vsim_gemm_set_streamk(int enable) { return gemm_set_streamk(enable); }
 int vsim_gemm_set_qk_pair(int mode) { return gemm_set_qk_pair(mode); }
+int vsim_gemm_set_tile_order(int cols) { return gemm_set_tile_order(cols); }
 int vsim_op_gemm_q4_256_pair(const void *w0, const void *w1, int M, int K, const void *x16, int n, float *y0, float *y1,
                              const double *cs, int d, int n_rot, int p0, void *stream) {
   if (!w0 || !w1 || !x16 || !y0 || !y1 || !cs || M <= 0 || K <= 0 || K % QK || p0 < 0 || n <= 0) {

@@ -317,6 +317,7 @@ int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, 
                             const G2Epi &e1, hipStream_t s);
 bool gemm_pair_enabled(int M, int K);
 int gemm_set_qk_pair(int mode);  // vsim_gemm_set_qk_pair (0 off, 1 default, 2 no split); returns the old setting
+int gemm_set_tile_order(int cols);  // vsim_gemm_set_tile_order; returns the old setting
 int gemm_set_streamk(int on);  // stream-K split of the register-dequant GEMM (default on); returns the old setting
 int gemm_release_stream(hipStream_t s);  // frees the stream-K workspace of (current device, s)
 int gemm_reserve_stream(hipStream_t s);  // the split workspace and kernel attributes, ahead of a prompt

@@ -689,6 +689,7 @@ constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
 // Hybrid split (PAIR launches, wg0 > 0): workgroups [0, wg0) take the whole tiles [0, wg0) (a
 // full round of the CUs), the rest run the split above over the tiles from t0 = wg0 on.
 struct RSk {
+  int cg = 0;           // tile order: column groups of cg tile-columns (0: one group, row-major)
   int upw = 0;          // units (K-tile pairs) per workgroup; 0: one tile per workgroup
   float *ws = nullptr;  // partials: [tile - t0][wave][32 f32x4][64 lanes]
   unsigned *flags = nullptr;
@@ -827,6 +828,23 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped loads past the end have landed
     __syncthreads();
   };
+  // tile t of the launch order -> its first row and column.  Column groups of sk.cg tile-columns,
+  // each walked row by row, so that the tiles an XCD runs at once (a contiguous range of t, below)
+  // span fewer columns: fewer activation slices streamed past the XCD's L2 per tile
+  // (PAIR: every tile of the first GEMM before the second's -- M % 256 == 0 -- so the hybrid
+  // split's remainder stays in the second weight)
+  auto tile_at = [&](int t, int &m0, int &n0) __attribute__((always_inline)) {
+    const int tmj = PAIR ? tm / 2 : tm, j = PAIR ? t / (tmj * tn) : 0;
+    t -= j * tmj * tn;
+    const int cg = sk.cg > 0 ? sk.cg : tn, per = tmj * cg, g = t / per, i = t - g * per;
+    m0 = j * M + (i / cg) * R_BM;
+    n0 = (g * cg + i % cg) * G2_BN;
+  };
+  // a contiguous range of `count` indices per XCD (workgroup b runs on XCD b % 8), in dispatch order
+  auto xcd_index = [&](int bid, int count) __attribute__((always_inline)) {
+    const int xcd = bid & 7, q8 = count >> 3, r8 = count & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  };
   auto epilogue = [&](int m0, int n0) __attribute__((always_inline)) {  // the wave's 32 rows x 256 columns
     if (PAIR && m0 >= M) {
       g2_epilogue<GQ, EM, 32, r_lds_bytes(), 256>(acc, m0 - M + 32 * wave, n0, M, N, bias, pr.y, gelu_tab, Q16, pr.epi,
@@ -838,9 +856,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
   };
   // one whole tile per workgroup, the first `count` tiles, XCD-remapped
   auto whole = [&](int count) __attribute__((always_inline)) {
-    const int bid = blockIdx.x, xcd = bid & 7, q8 = count >> 3, r8 = count & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int m0 = (wg / tn) * R_BM, n0 = (wg % tn) * G2_BN;
+    int m0, n0;
+    tile_at(xcd_index(blockIdx.x, count), m0, n0);
     run(m0, n0, 0, nk);
     epilogue(m0, n0);
   };
@@ -856,14 +873,18 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     // must not be hoisted above the first's K loop (the counted waits allow no spill traffic).
     const int nu = nk / 2;
     const int t0 = PAIR ? sk.t0 : 0;  // (tile indices below count from t0)
-    const int u0 = ((int)blockIdx.x - (PAIR ? sk.wg0 : 0)) * sk.upw, u1 = min(u0 + sk.upw, (nwg - t0) * nu);
+    // (split workgroups XCD-remapped like whole tiles: a tile's pieces run on one XCD; wg0 % 8 == 0)
+    const int nsp = (int)gridDim.x - (PAIR ? sk.wg0 : 0);
+    const int u0 = xcd_index((int)blockIdx.x - (PAIR ? sk.wg0 : 0), nsp) * sk.upw, u1 = min(u0 + sk.upw, (nwg - t0) * nu);
     const int tA = u0 / nu, aA = u0 - tA * nu, eA = min(u1 - tA * nu, nu);
     const int eB = max(u1 - (tA + 1) * nu, 0);  // units of tA + 1 from its start
     // first: the piece that starts a tile and is finished by the next workgroup (published)
     const bool pubA = aA == 0 && eA < nu, pubB = eB > 0 && eB < nu;
     if (pubA || pubB) {
       const int t = pubA ? tA : tA + 1, e = pubA ? eA : eB;
-      run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 0, 2 * e);
+      int m0, n0;
+      tile_at(t + t0, m0, n0);
+      run(m0, n0, 0, 2 * e);
       float *wp = sk.ws + ((size_t)(t * 8 + wave) * 32 * 64 + lane) * 4;
       // (4 stores per base address, offsets 0-3 KB)
 #pragma unroll
@@ -889,7 +910,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
     const bool finA = !pubA;
     const int t = finA ? tA : tA + 1, a = finA ? aA : 0, e = finA ? eA : eB;
     if (!finA && e < nu) return;
-    run(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN, 2 * a, 2 * (e - a));
+    int m0, n0;
+    tile_at(t + t0, m0, n0);
+    run(m0, n0, 2 * a, 2 * (e - a));
     if (a > 0) {  // the earlier part's partial
       if (tid == 0) {
         unsigned spins = 0;
@@ -920,7 +943,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm_q4r(const W4 WQ, int M, 
         for (int q = 0; q < 4; ++q) acc[g >> 2][4 * (g & 3) + q] = pv[q] + acc[g >> 2][4 * (g & 3) + q];
       }
     }
-    epilogue(((t + t0) / tn) * R_BM, ((t + t0) % tn) * G2_BN);
+    epilogue(m0, n0);
   }
 }
 
@@ -938,6 +961,14 @@ int gemm_set_streamk(int on) {
   g_streamk = on ? 1 : 0;
   return was;
 }
+
+static int g_tile_cols = 4;  // vsim_gemm_set_tile_order
+int gemm_set_tile_order(int cols) {
+  const int was = g_tile_cols;
+  g_tile_cols = cols < 0 ? 0 : cols;
+  return was;
+}
+static int tile_cg(int tn) { return g_tile_cols > 0 && tn % g_tile_cols == 0 ? g_tile_cols : 0; }
 
 static std::mutex g_sk_mu;
 static std::map<std::pair<int, hipStream_t>, SkWs> g_sk_ws;  // (device, stream): a null stream is per device
@@ -1035,6 +1066,7 @@ static int r_go(const W4 &WQ, int M, int K, const void *x16, int n, const float 
                 void *q16, const G2Epi &epi, hipStream_t s) {
   const int nwg = ((M + R_BM - 1) / R_BM) * ((n + G2_BN - 1) / G2_BN);
   RSk sk;
+  sk.cg = tile_cg((n + G2_BN - 1) / G2_BN);
   int grid = nwg;
   const int nu = K / G2_BK / 2;
   // (grids of at least half the CUs: each tile in at most two pieces.  GPT-J-6B's 128-tile
@@ -1132,6 +1164,7 @@ int launch_gemm_q4_256_pair(const W4 &W0, const W4 &W1, const void *x16, int n, 
   pr.epi = e1;
   const int nwg = 2 * (M / R_BM) * ((n + G2_BN - 1) / G2_BN), nu = K / G2_BK / 2;
   RSk sk;
+  sk.cg = tile_cg((n + G2_BN - 1) / G2_BN);
   // hybrid split: the whole rounds as whole tiles, the remainder split over one round of CUs
   const int cus = device_cus();
   const int wg0 = nwg / cus * cus, rest = nwg - wg0;

@@ -50,22 +50,28 @@ __device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::
 // scalar loads.
 constexpr int C2_CB = 8, C2_CP = C2_CB * 16, C2_LD = C2_CP + 4, C2_NPW = C2_CB / 2;
 constexpr int C2_THREADS = 64 * (1 + C2_NPW);
-constexpr int C2_RING = 3, C2_WIN = 16, C2_DEPTH = 4, C2_RAW = C2_DEPTH;  // raw slot reuse: see below
+// DEPTH: chunks of weights and factors in flight by LDS-DMA (and raw LDS slots).  k_layer_tail
+// runs 8 (r04 A/B, tools/tail_ab.sh: tail 38.9-39.0 vs 39.7-39.8 us at 4, 40.1-40.2 at 6, 40.3-40.4
+// at 10; 541-542 vs 534-535 tok/s); k_gemv_chain32 keeps 4, so two workgroups still fit a CU.
+constexpr int C2_RING = 3, C2_WIN = 16, C2_DEPTH_GEMV = 4, C2_DEPTH_TAIL = 8;
 // s_waitcnt vmcnt(n) alone (expcnt, lgkmcnt at their maxima): n's low 4 bits in [3:0], high 2 in [15:14]
 constexpr int waitcnt_vm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
-constexpr int C2_WAIT_VM3 = waitcnt_vm(3 * (C2_DEPTH - 2));  // wave 1: nibbles, scales, factors
-constexpr int C2_WAIT_VM2 = waitcnt_vm(2 * (C2_DEPTH - 2));  // other producers: nibbles, scales
-static_assert(3 * (C2_DEPTH - 2) < 64, "vmcnt immediate");
 
+template <int DEPTH>
 struct C2Lds {
   float P[C2_RING][32 * C2_LD];
-  uint4 RQ[C2_RAW][C2_NPW][64];
-  float RD[C2_RAW][C2_NPW][64];
-  float RX[C2_RAW][C2_CB * QK];
+  uint4 RQ[DEPTH][C2_NPW][64];
+  float RD[DEPTH][C2_NPW][64];
+  float RX[DEPTH][C2_CB * QK];
 };
 
 // tile t of the batch's jobs (blockIdx.x in k_gemv_chain32, a role offset in k_layer_tail)
-__device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds &L) {
+template <int DEPTH>
+__device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DEPTH> &L) {
+  constexpr int C2_RAW = DEPTH;  // raw slot reuse: see below
+  constexpr int C2_WAIT_VM3 = waitcnt_vm(3 * (DEPTH - 2));  // wave 1: nibbles, scales, factors
+  constexpr int C2_WAIT_VM2 = waitcnt_vm(2 * (DEPTH - 2));  // other producers: nibbles, scales
+  static_assert(3 * (DEPTH - 2) < 64, "vmcnt immediate");
   auto &P = L.P;
   auto &RQ = L.RQ;
   auto &RD = L.RD;
@@ -124,7 +130,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds &L
     int ps = 0;
     auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const uint4 &qc, float dqc, uint4 &qn, float &dqn) {
       ldraw(k + 1, qn, dqn, xn);
-      dma(k + C2_DEPTH);
+      dma(k + DEPTH);
       {
         const float dv = k * C2_CB + o < nb ? dqc : 0.0f;
         const f32x2 d2 = {512.0f * dv, 512.0f * dv}, m2 = {-8.0f * dv, -8.0f * dv};
@@ -145,7 +151,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds &L
       __syncthreads();
     };
 #pragma unroll
-    for (int c = 0; c < C2_DEPTH; ++c) dma(c);
+    for (int c = 0; c < DEPTH; ++c) dma(c);
     f32x2 xa[16], xb[16];
     uint4 qa, qb;
     float da, db;
@@ -214,7 +220,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds &L
 }
 
 __global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
-  __shared__ C2Lds L;
+  __shared__ C2Lds<C2_DEPTH_GEMV> L;
   chain32_body(B, blockIdx.x, L);
 }
 
@@ -245,8 +251,8 @@ struct TailJob {
 
 __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
   __shared__ union {
-    C2Lds g;
-    float a[sizeof(C2Lds) / sizeof(float)];
+    C2Lds<C2_DEPTH_TAIL> g;
+    float a[sizeof(C2Lds<C2_DEPTH_TAIL>) / sizeof(float)];
   } L;
   int b = blockIdx.x;
   if (b < T.nf) {
@@ -282,7 +288,7 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
                       hipStream_t s) {
   const int S = a.nsplit > 1 ? a.nsplit : 1;
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
-      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds)) {
+      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds<C2_DEPTH_TAIL>)) {
     set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
     return VSIM_EINVAL;
   }
@@ -296,8 +302,9 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   for (int i = 0; i < f.nj; ++i) T.nf += f.j[i].w.tiles;
   int no = 0;
   for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;
-  // dynamic LDS pad: above half the CU's LDS, so one workgroup per CU (fc_out's consumer
-  // keeps its SIMD); the workgroups that find no CU start as attention heads end
+  // one workgroup per CU (fc_out's consumer keeps its SIMD): the static LDS is above half the
+  // CU's already at DEPTH 8, the dynamic pad keeps it so at any depth; the workgroups that find
+  // no CU start as attention heads end
   hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H * S + no), dim3(C2_THREADS), 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;

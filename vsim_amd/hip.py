@@ -32,7 +32,7 @@ EXPORTS = [
     "vsim_op_act_quant_f16", "vsim_op_gemm_f16_gelu_q", "vsim_op_gemm_f16_rope", "vsim_op_gemm_f16_join",
     "vsim_op_gemm_q4_256", "vsim_op_get_rows",
     "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv",
-    "vsim_op_attn_prefill", "vsim_op_attn_prefill_q16", "vsim_gemm_set_streamk", "vsim_gemm_set_qk_pair", "vsim_op_gemm_q4_256_pair", "vsim_op_norm_f16q",
+    "vsim_op_attn_prefill", "vsim_op_attn_prefill_q16", "vsim_gemm_set_streamk", "vsim_gemm_set_qk_pair", "vsim_gemm_set_tile_order", "vsim_op_gemm_q4_256_pair", "vsim_op_norm_f16q",
     "vsim_op_tables",
     "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_get_tensor",
     "vsim_model_randomize",
@@ -131,6 +131,7 @@ def lib():
     L.vsim_op_attn_prefill_q16.argtypes = [vp, vp, vp, ci, ci, ci, ci, cf, vp, vp]
     L.vsim_gemm_set_streamk.argtypes = [ci]
     L.vsim_gemm_set_qk_pair.argtypes = [ci]
+    L.vsim_gemm_set_tile_order.argtypes = [ci]
     L.vsim_op_gemm_q4_256_pair.argtypes = [vp, vp, ci, ci, vp, ci, vp, vp, vp, ci, ci, ci, vp]
     L.vsim_op_norm_f16q.argtypes = [vp, ci, ci, vp, vp, vp, vp]
     L.vsim_op_tables.argtypes = [vp, vp]
