@@ -43,33 +43,57 @@ __device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::
 // ================================================================== 32-row variant
 // Same chain and producer/consumer protocol for one W4T32 tile (32 rows) per workgroup, so a
 // job with few rows spreads over more CUs (fc_out: 128 workgroups instead of 64) and each
-// CU's producers carry half the work.  4 producer waves, each 2 blocks of the 8-block chunk
-// (lanes 0-31: rows of block 2p, lanes 32-63: rows of block 2p+1); the activation factors
-// then differ between the two half-waves, so they come through the LDS ring as well (one
-// LDS-DMA per chunk by the first producer, read with per-half broadcast loads) instead of
-// scalar loads.
-constexpr int C2_CB = 8, C2_CP = C2_CB * 16, C2_LD = C2_CP + 4, C2_NPW = C2_CB / 2;
-constexpr int C2_THREADS = 64 * (1 + C2_NPW);
-// DEPTH: chunks of weights and factors in flight by LDS-DMA (and raw LDS slots).  k_layer_tail
-// runs 8 (r04 A/B, tools/tail_ab.sh: tail 38.9-39.0 vs 39.7-39.8 us at 4, 40.1-40.2 at 6, 40.3-40.4
-// at 10; 541-542 vs 534-535 tok/s); k_gemv_chain32 keeps 4, so two workgroups still fit a CU.
-constexpr int C2_RING = 3, C2_WIN = 16, C2_DEPTH_GEMV = 4, C2_DEPTH_TAIL = 8;
+// CU's producers carry half the work.  Producer waves take 2 blocks of the chunk each (lanes
+// 0-31: rows of block 2p, lanes 32-63: rows of block 2p+1); the activation factors then differ
+// between the two half-waves, so they come through the LDS ring as well (LDS-DMA of 1 KB pieces
+// per chunk by the first producers, read with per-half broadcast loads) instead of scalar loads.
+// Shapes (C2Shape): 8-block chunks, 4 producers, the fourth (wave 4) on the consumer's SIMD,
+// for k_gemv_chain32 and k_layer_tail (LDS-DMA depth 4 and 8).  FILL leaves the consumer's SIMD
+// to the consumer (waves 4, 8, ... only join the barriers).  r04 per-chunk s_memtime stamps of the
+// tail's fc_out tiles (tools/variants/mk_tail_stamps.py, profiles/r04_tail_stamps*.txt): a step of
+// ~1,600 cycles, the consumer's 128 adds 1,308 of them (10.2 cycles per add against the 4.63 of a
+// dependent add alone); with 12-block chunks, 6 producers and the consumer alone on SIMD0 still
+// 9.4 per add (the producers then waited 830-880 cycles a step at the barrier) and the tail 41.4
+// vs 38.8 us: the consumer loop itself, not the producer beside it, set the step.  Its LDS reads
+// issued one per 4 adds cost that; issued in groups of 4 after 16 adds (one lgkmcnt wait per
+// group), the tail took 36.3 vs 39.0 us (574-576 vs 550-551 tok/s; groups of 8 the same).
 // s_waitcnt vmcnt(n) alone (expcnt, lgkmcnt at their maxima): n's low 4 bits in [3:0], high 2 in [15:14]
 constexpr int waitcnt_vm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+// waves for NPW producers when the waves on the consumer's SIMD (4, 8, ...) are left idle
+constexpr int c2_waves(int npw, bool fill) {
+  int w = 1, p = 0;
+  while (p < npw) p += (!fill || w % 4 != 0) ? 1 : 0, ++w;
+  return w;
+}
+template <int CB_, int DEPTH_, bool FILL_>
+struct C2Shape {
+  static constexpr int CB = CB_, CP = CB * 16, LD = CP + 4, NPW = CB / 2, DEPTH = DEPTH_;
+  static constexpr bool FILL = FILL_;
+  static constexpr int THREADS = 64 * c2_waves(NPW, FILL);
+  static constexpr int XP = (CB + 7) / 8;  // 1 KB factor pieces per chunk (8 blocks each)
+  static_assert(CB % 2 == 0 && XP <= NPW && CP / 4 % 16 == 0, "chunk shape");
+};
+constexpr int C2_RING = 3, C2_WIN = 16;
+// DEPTH: chunks of weights and factors in flight by LDS-DMA (and raw LDS slots).  r04 A/B of the
+// 8-block tail (tools/tail_ab.sh): tail 38.9-39.0 us at 8 vs 39.7-39.8 at 4, 40.1-40.2 at 6,
+// 40.3-40.4 at 10.  k_gemv_chain32 keeps 4, so two workgroups still fit a CU.
+using C2Gemv = C2Shape<8, 4, false>;
+using C2Tail = C2Shape<8, 8, false>;
 
-template <int DEPTH>
+template <class S>
 struct C2Lds {
-  float P[C2_RING][32 * C2_LD];
-  uint4 RQ[DEPTH][C2_NPW][64];
-  float RD[DEPTH][C2_NPW][64];
-  float RX[DEPTH][C2_CB * QK];
+  float P[C2_RING][32 * S::LD];
+  uint4 RQ[S::DEPTH][S::NPW][64];
+  float RD[S::DEPTH][S::NPW][64];
+  float RX[S::DEPTH][S::XP * 8 * QK];
 };
 
 // tile t of the batch's jobs (blockIdx.x in k_gemv_chain32, a role offset in k_layer_tail)
-template <int DEPTH>
-__device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DEPTH> &L) {
+template <class S>
+__device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<S> &L) {
+  constexpr int DEPTH = S::DEPTH, CB = S::CB, CP = S::CP, LD = S::LD;
   constexpr int C2_RAW = DEPTH;  // raw slot reuse: see below
-  constexpr int C2_WAIT_VM3 = waitcnt_vm(3 * (DEPTH - 2));  // wave 1: nibbles, scales, factors
+  constexpr int C2_WAIT_VM3 = waitcnt_vm(3 * (DEPTH - 2));  // factor-piece producers: nibbles, scales, factors
   constexpr int C2_WAIT_VM2 = waitcnt_vm(2 * (DEPTH - 2));  // other producers: nibbles, scales
   static_assert(3 * (DEPTH - 2) < 64, "vmcnt immediate");
   auto &P = L.P;
@@ -86,12 +110,16 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
   }
   if (ji >= B.nj) return;
   ji = __builtin_amdgcn_readfirstlane(ji);
-  const int nb = B.j[ji].w.k / QK, nch = (nb + C2_CB - 1) / C2_CB;
+  const int nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
   const int nit = (nch + 2 + 1) & ~1;
   const uint8_t *tqs = B.j[ji].w.qs + (size_t)t * nb * T32 * 16;
   const float *td = B.j[ji].w.d + (size_t)t * nb * T32;
   const float *x = B.j[ji].xd;
 
+  if (S::FILL && wave > 0 && wave % 4 == 0) {  // the consumer's SIMD: barriers only
+    for (int k = 0; k < nit + 2; ++k) __syncthreads();
+    return;
+  }
   if (wave > 0) {
     // ------------------------------------------------------------- producer
     // Step k: read chunk k+1's raw block and factors (landed before the
@@ -99,28 +127,29 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
     // the registers filled in step k-1, wait for this wave's DMA of chunk k+2, barrier.
     // Raw slot reuse: chunk c lives in slot c % RAW; the DMA of chunk k+DEPTH (step k) reuses
     // the slot of chunk k, whose registers were read in step k-1 (retired at that barrier).
-    const int p = wave - 1, r = lane & 31, hb = lane >> 5;
+    const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
     const int o = 2 * p + hb;  // this lane's block within the chunk
+    const bool xp = p < S::XP;  // this wave also brings a 1 KB piece of the chunk's factors
     const uint8_t *qs = tqs + (size_t)r * 16;
     const float *dd = td + r;
     auto dma = [&](int c) {
       const int slot = c % C2_RAW;
-      const int b = min(c * C2_CB + o, nb - 1);
+      const int b = min(c * CB + o, nb - 1);
       glds16(qs + (size_t)b * (T32 * 16), lds_addr(&RQ[slot][p][0]));
       glds4(dd + (size_t)b * T32, lds_addr(&RD[slot][p][0]));
-      if (p == 0) {  // the chunk's 8 x 32 activation factors, 16 bytes per lane (clamped block)
-        const int bx = min(c * C2_CB + (lane >> 3), nb - 1);
-        glds16(x + (size_t)bx * QK + 4 * (lane & 7), lds_addr(&RX[slot][0]));
+      if (xp) {  // 8 blocks x 32 factors, 16 bytes per lane (clamped block)
+        const int bx = min(c * CB + 8 * p + (lane >> 3), nb - 1);
+        glds16(x + (size_t)bx * QK + 4 * (lane & 7), lds_addr(&RX[slot][256 * p]));
       }
     };
     auto ldraw = [&](int c, uint4 &q, float &dq, f32x2 *xv) {
       const int slot = c % C2_RAW;
       q = RQ[slot][p][lane];
       dq = RD[slot][p][lane];
-      const float4 *xp = (const float4 *)&RX[slot][o * QK];
+      const float4 *xq = (const float4 *)&RX[slot][o * QK];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float4 v = xp[i];
+        const float4 v = xq[i];
         xv[2 * i].x = v.x;
         xv[2 * i].y = v.y;
         xv[2 * i + 1].x = v.z;
@@ -132,9 +161,9 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
       ldraw(k + 1, qn, dqn, xn);
       dma(k + DEPTH);
       {
-        const float dv = k * C2_CB + o < nb ? dqc : 0.0f;
+        const float dv = k * CB + o < nb ? dqc : 0.0f;
         const f32x2 d2 = {512.0f * dv, 512.0f * dv}, m2 = {-8.0f * dv, -8.0f * dv};
-        float *dst = &P[ps][r * C2_LD + o * 16];
+        float *dst = &P[ps][r * LD + o * 16];
         const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
 #pragma unroll
         for (int wv = 0; wv < 4; ++wv) {
@@ -144,7 +173,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
         }
       }
       ps = ps == C2_RING - 1 ? 0 : ps + 1;
-      if (p == 0)  // this wave's DMA of chunk k+2 landed
+      if (xp)  // this wave's DMA of chunk k+2 landed
         __builtin_amdgcn_s_waitcnt(C2_WAIT_VM3);
       else
         __builtin_amdgcn_s_waitcnt(C2_WAIT_VM2);
@@ -155,7 +184,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
     f32x2 xa[16], xb[16];
     uint4 qa, qb;
     float da, db;
-    if (p == 0)  // chunks 0 and 1 landed
+    if (xp)  // chunks 0 and 1 landed
       __builtin_amdgcn_s_waitcnt(C2_WAIT_VM3);
     else
       __builtin_amdgcn_s_waitcnt(C2_WAIT_VM2);
@@ -173,7 +202,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
   float acc = 0.0f;
   float4 win[C2_WIN];
   const int lr = lane & 31;
-  auto src = [&](int c) { return &P[c % C2_RING][lr * C2_LD]; };
+  auto src = [&](int c) { return &P[c % C2_RING][lr * LD]; };
   __builtin_amdgcn_s_setprio(3);
   __syncthreads();
   __syncthreads();
@@ -186,16 +215,22 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
     } else if (c >= 0 && c < nch) {
       const float *pc = src(c), *pn = src(c + 1);
 #pragma unroll
-      for (int j = 0; j < C2_CP / 4; ++j) {
-        const float4 v = win[j % C2_WIN];
-        acc = acc + v.x;
-        acc = acc + v.y;
-        acc = acc + v.z;
-        acc = acc + v.w;
-        const int jn = j + C2_WIN;
-        win[j % C2_WIN] = jn < C2_CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - C2_CP / 4));
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      for (int j0 = 0; j0 < CP / 4; j0 += 4) {
+#pragma unroll
+        for (int j = j0; j < j0 + 4; ++j) {
+          const float4 v = win[j % C2_WIN];
+          acc = acc + v.x;
+          acc = acc + v.y;
+          acc = acc + v.z;
+          acc = acc + v.w;
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + 4; ++j) {
+          const int jn = j + C2_WIN;
+          win[j % C2_WIN] = jn < CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - CP / 4));
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
       }
     }
     __syncthreads();
@@ -219,8 +254,8 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<DE
   }
 }
 
-__global__ void __launch_bounds__(C2_THREADS, 2) k_gemv_chain32(GemvBatch B) {
-  __shared__ C2Lds<C2_DEPTH_GEMV> L;
+__global__ void __launch_bounds__(C2Gemv::THREADS, 2) k_gemv_chain32(GemvBatch B) {
+  __shared__ C2Lds<C2Gemv> L;
   chain32_body(B, blockIdx.x, L);
 }
 
@@ -249,10 +284,10 @@ struct TailJob {
   int nf;
 };
 
-__global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
+__global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   __shared__ union {
-    C2Lds<C2_DEPTH_TAIL> g;
-    float a[sizeof(C2Lds<C2_DEPTH_TAIL>) / sizeof(float)];
+    C2Lds<C2Tail> g;
+    float a[sizeof(C2Lds<C2Tail>) / sizeof(float)];
   } L;
   int b = blockIdx.x;
   if (b < T.nf) {
@@ -262,7 +297,7 @@ __global__ void __launch_bounds__(C2_THREADS, 1) k_layer_tail(TailJob T) {
   b -= T.nf;
   const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
   if (b < na) {
-    attn_body<C2_THREADS>(T.a, b, L.a);
+    attn_body<C2Tail::THREADS>(T.a, b, L.a);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's output stores
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -288,7 +323,7 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
                       hipStream_t s) {
   const int S = a.nsplit > 1 ? a.nsplit : 1;
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
-      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds<C2_DEPTH_TAIL>)) {
+      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds<C2Tail>)) {
     set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
     return VSIM_EINVAL;
   }
@@ -305,7 +340,7 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   // one workgroup per CU (fc_out's consumer keeps its SIMD): the static LDS is above half the
   // CU's already at DEPTH 8, the dynamic pad keeps it so at any depth; the workgroups that find
   // no CU start as attention heads end
-  hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H * S + no), dim3(C2_THREADS), 8192, s, T);
+  hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H * S + no), dim3(C2Tail::THREADS), 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -523,7 +558,7 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)), dim3(64 * SoloShape<SOLO_CB, 1>::WAVES),
                        0, s, B);
   } else {
-    hipLaunchKernelGGL(k_gemv_chain32, dim3(tiles), dim3(C2_THREADS), 0, s, B);
+    hipLaunchKernelGGL(k_gemv_chain32, dim3(tiles), dim3(C2Gemv::THREADS), 0, s, B);
   }
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
