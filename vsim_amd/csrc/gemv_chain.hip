@@ -366,7 +366,9 @@ struct SoloShape {
   // the rest only join the barriers; the others are the producers
   static constexpr int WAVES = PRODUCERS + (PRODUCERS + 2) / 3;  // a 0-mod-4 slot per 3 producers
   static constexpr int ROWS = 64 * CONS;
-  static constexpr int WIN = 12;  // (r04: 12 and chain32's 16 read deeper than r03's 8: tail -1.1 us)
+  // (r04: 12 and chain32's 16 read deeper than r03's 8: tail -1.1 us.  The reads go in groups of
+  // 6 after 24 adds, as chain32's in groups of 4: batch 21.9 vs 22.4 us, lm_head 37.6-37.8 vs 38.6)
+  static constexpr int WIN = 12;
   static_assert(CP / 4 % WIN == 0, "the read window must tile the chunk");
   static_assert(WAVES <= 16, "workgroup size");
   static_assert((WAVES + 3) / 4 >= CONS, "consumer waves on one SIMD");
@@ -487,16 +489,22 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
     } else if (c >= 0 && c < nch) {
       const float *pc = src(c), *pn = src(c + 1);
 #pragma unroll
-      for (int j = 0; j < S::CP / 4; ++j) {
-        const float4 v = win[j % S::WIN];
-        acc = acc + v.x;
-        acc = acc + v.y;
-        acc = acc + v.z;
-        acc = acc + v.w;
-        const int jn = j + S::WIN;
-        win[j % S::WIN] = jn < S::CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - S::CP / 4));
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU x4
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read x1
+      for (int j0 = 0; j0 < S::CP / 4; j0 += 6) {
+#pragma unroll
+        for (int j = j0; j < j0 + 6; ++j) {
+          const float4 v = win[j % S::WIN];
+          acc = acc + v.x;
+          acc = acc + v.y;
+          acc = acc + v.z;
+          acc = acc + v.w;
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + 6; ++j) {
+          const int jn = j + S::WIN;
+          win[j % S::WIN] = jn < S::CP / 4 ? *(const float4 *)(pc + 4 * jn) : *(const float4 *)(pn + 4 * (jn - S::CP / 4));
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);  // VALU x24
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS read x6
       }
     }
     __syncthreads();
