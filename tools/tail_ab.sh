@@ -13,7 +13,7 @@ for i in 1 2; do
     name=${v%+bidx}
     [ "$name" != "$v" ] && export VSIM_TAIL_BLOCKIDX=1
     [ "$name" != product ] && export VSIM_LIB=$root/vsim_amd/_build/var/$name.so
-    timeout -k 10 300 python3 "$root/bench.py" --no-cpu-baseline --no-pipeline-20b --no-fast --steps 128 > "$out/tail_ab_$v$i.log" 2>&1 || exit 2
+    timeout -k 10 300 python3 "$root/bench.py" --no-cpu-baseline --no-pipeline-20b --no-fast --steps ${STEPS:-128} > "$out/tail_ab_$v$i.log" 2>&1 || exit 2
     python3 -c "
 import json
 d=json.loads([l for l in open('$out/tail_ab_$v$i.log') if l.startswith('{')][-1])

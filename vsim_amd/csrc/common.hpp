@@ -280,6 +280,7 @@ int launch_act_quant_f16(const float *x, int K, int n, const float *bias, bool g
 int launch_gemm_f16x(const W4 &W, const void *x16, int n, const float *bias, float *y, hipStream_t s);
 // long prompts: fp16 weight images (launch_w4_expand_f16: [M][K], 2 bytes per weight) and the
 // 256 x 256-tile GEMM on them (K % 64 == 0), same operand values as launch_gemm_f16x
+constexpr int EXACT_GEMV_MAX_N = 32;  // exact prompt batches up to this many tokens run as batched decode GEMVs (ops_q4.hip)
 constexpr int G2_MIN_N = 256;
 int launch_w4_expand_f16(const W4 &W, void *out, hipStream_t s);
 // q16 non-null: y is not written; bias + GELU + Q4_0 quantize of the result into q16 ([n][M]

@@ -10,6 +10,8 @@
 // tile the 16-byte nibble blocks are stored block-major, so the 32 rows' block b sit in
 // 512 contiguous bytes and the 32 scales of block b in 128 contiguous bytes.  A wave whose
 // lanes own rows reads whole cache lines; bytes per weight stay 0.625.
+#include <algorithm>
+
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
 
@@ -222,20 +224,27 @@ int launch_q4_gemv(const void *w, int M, int K, const void *xq, const float *xd,
   if (mode == VSIM_MODE_EXACT && !xd) { set_error("q4_gemv: exact mode needs xd"); return VSIM_EINVAL; }
   // fast mode, prompt batches: fp16 MFMA GEMM after in-LDS dequant (gemm_f16.hip)
   if (mode == VSIM_MODE_FAST && n >= GEMM_MIN_N) return launch_gemm_q4_f16(W, xq, n, bias, y, s);
-  // exact mode, prompt batches: the register-tiled chain GEMM (gemm_exact.hip)
-  if (mode == VSIM_MODE_EXACT && n > 1) return launch_gemm_exact(W, xd, n, bias, y, s);
+  // exact mode, prompt batches: the register-tiled chain GEMM (gemm_exact.hip).  Its 128-token
+  // tiles cost the same for 5 tokens as for 128 (r04 rocprof: 1.09 ms per GPT-J GEMM for a
+  // 5-token prompt), so short batches take the decode GEMV, up to 4 tokens per launch (one job
+  // each: the same chains, bit for bit)
+  if (mode == VSIM_MODE_EXACT && n > EXACT_GEMV_MAX_N) return launch_gemm_exact(W, xd, n, bias, y, s);
   const size_t nbk = (size_t)n * (K / QK);
   const uint8_t *xqs = (const uint8_t *)xq;
   const float *xdd = (const float *)(xqs + nbk * 16);
-  for (int ic = 0; ic < n; ++ic) {
+  const int per = mode == VSIM_MODE_EXACT ? 4 : 1;
+  for (int i0 = 0; i0 < n; i0 += per) {
     GemvBatch B{};
-    B.nj = 1;
-    B.j[0].w = W;
-    B.j[0].xd = xd ? xd + (size_t)ic * K : nullptr;
-    B.j[0].xqs = xqs + (size_t)ic * (K / QK) * 16;
-    B.j[0].xdd = xdd + (size_t)ic * (K / QK);
-    B.j[0].bias = bias;
-    B.j[0].y = y + (size_t)ic * M;
+    B.nj = std::min(per, n - i0);
+    for (int u = 0; u < B.nj; ++u) {
+      const int ic = i0 + u;
+      B.j[u].w = W;
+      B.j[u].xd = xd ? xd + (size_t)ic * K : nullptr;
+      B.j[u].xqs = xqs + (size_t)ic * (K / QK) * 16;
+      B.j[u].xdd = xdd + (size_t)ic * (K / QK);
+      B.j[u].bias = bias;
+      B.j[u].y = y + (size_t)ic * M;
+    }
     if (int rc = launch_gemv_batch(B, mode, s)) return rc;
   }
   return VSIM_OK;
