@@ -139,7 +139,7 @@ __device__ __forceinline__ void chain32_body(const GemvBatch &B, int t, C2Lds<S>
       glds4(dd + (size_t)b * T32, lds_addr(&RD[slot][p][0]));
       if (xp) {  // 8 blocks x 32 factors, 16 bytes per lane (clamped block)
         const int bx = min(c * CB + 8 * p + (lane >> 3), nb - 1);
-        glds16(x + (size_t)bx * QK + 4 * (lane & 7), lds_addr(&RX[slot][256 * p]));
+        glds16_sc1(x + (size_t)bx * QK + 4 * (lane & 7), lds_addr(&RX[slot][256 * p]));
       }
     };
     auto ldraw = [&](int c, uint4 &q, float &dq, f32x2 *xv) {
@@ -265,8 +265,14 @@ __global__ void __launch_bounds__(C2Gemv::THREADS, 2) k_gemv_chain32(GemvBatch B
 // longest dependency, instead of before it.  Roles by workgroup index:
 //   [0, nf)          fc_out tiles (32-row chain GEMV)
 //   [nf, nf + na)    attention heads (attn.hpp with this kernel's 5 waves); each head
-//                    releases its output and counts itself in *done (agent scope)
-//   [nf + na, ...)   out-projection tiles; wait until *done == na, then acquire
+//                    stores the out-projection's operand write-through (sc1, CO = true),
+//                    drains them (vmcnt) and counts itself in *done (agent scope)
+//   [nf + na, ...)   out-projection tiles; wait until *done == na; their factor LDS-DMA is sc1
+//                    (device-coherent: it reads past stale lines in the XCD's L2), so neither
+//                    side needs a fence.  r04: the release fence (an L2 write-back per head)
+//                    and the acquire (an L2 invalidate, which also dropped fc_out's lines)
+//                    cost 38.9 vs 35.8-36.0 us per tail at the bench's 248 positions
+//                    (profiles/r04_tail_headpath_ab.txt)
 // Waiting workgroups only wait for lower-indexed ones, which the dispatcher places first on
 // this part (and fc_out's tiles never wait, so the CUs they hold always come free); the wait
 // is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it the error counter
@@ -297,8 +303,8 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   b -= T.nf;
   const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
   if (b < na) {
-    attn_body<C2Tail::THREADS>(T.a, b, L.a);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's output stores
+    attn_body<C2Tail::THREADS, true>(T.a, b, L.a);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through output stores landed
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -315,7 +321,6 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   chain32_body(T.o, b, L.g);
 }
 
