@@ -6,7 +6,7 @@ root=$(cd "$(dirname "$0")/.." && pwd); out=$root/gpurun_out; mkdir -p "$out"; c
 for v in "$@"; do
   unset VSIM_LIB; [ $v != product ] && export VSIM_LIB=$root/vsim_amd/_build/var/$v.so
   timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
-    "$root/tests/test_gpu_fullwidth.py" -k "gpt-j or bloom" > "$out/r04_par_$v.log" 2>&1
+    "$root/tests/test_gpu_fullwidth.py" -k "${PARITY_K:-gpt-j or bloom}" > "$out/r04_par_$v.log" 2>&1
   rc=$?; echo "[$v] parity exit=$rc $(grep -E 'passed|failed' "$out/r04_par_$v.log" | tail -1)"
   [ "$rc" -gt 1 ] && exit $rc
 done

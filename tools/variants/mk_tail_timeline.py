@@ -51,7 +51,7 @@ g = rep(g, """  int b = blockIdx.x;
     tl_mark(wg, 1);
     return;
   }""")
-g = rep(g, """    attn_body<C2Tail::THREADS>(T.a, b, L.a);""", """    attn_body<C2Tail::THREADS>(T.a, b, L.a, wg);""")
+g = rep(g, """    attn_body<C2Tail::THREADS, true>(T.a, b, L.a);""", """    attn_body<C2Tail::THREADS, true>(T.a, b, L.a, wg);""")
 g = rep(g, """    if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
@@ -61,8 +61,8 @@ g = rep(g, """    if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATO
   }
   b -= na;
   tl_mark(wg, 0);""")
-g = rep(g, """  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  chain32_body(T.o, b, L.g);""", """  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+g = rep(g, """  __syncthreads();
+  chain32_body(T.o, b, L.g);""", """  __syncthreads();
   tl_mark(wg, 1);
   chain32_body(T.o, b, L.g);
   __syncthreads();
