@@ -48,8 +48,8 @@ __device__ __forceinline__ void producer_barrier() { asm volatile("s_barrier" ::
 // between the two half-waves, so they come through the LDS ring as well (LDS-DMA of 1 KB pieces
 // per chunk by the first producers, read with per-half broadcast loads) instead of scalar loads.
 // Shapes (C2Shape): k_gemv_chain32: 8-block chunks, 4 producers, the fourth (wave 4) on the
-// consumer's SIMD, LDS-DMA depth 4; k_layer_tail: 12-block chunks, 6 producers, FILL (the
-// consumer's SIMD left to the consumer: waves 4, 8, ... only join the barriers), depth 4.  r04 per-chunk s_memtime stamps of the
+// consumer's SIMD, LDS-DMA depth 4; k_layer_tail: 16-block chunks, 8 producers, FILL (the
+// consumer's SIMD left to the consumer: waves 4, 8 only join the barriers), depth 4.  r04 per-chunk s_memtime stamps of the
 // tail's fc_out tiles (tools/variants/mk_tail_stamps.py, profiles/r04_tail_stamps*.txt): a step of
 // ~1,600 cycles, the consumer's 128 adds 1,308 of them (10.2 cycles per add against the 4.63 of a
 // dependent add alone); with 12-block chunks, 6 producers and the consumer alone on SIMD0 still
@@ -77,11 +77,13 @@ constexpr int C2_RING = 3, C2_WIN = 16;
 // DEPTH: chunks of weights and factors in flight by LDS-DMA (and raw LDS slots).  r04 A/B of the
 // 8-block tail (tools/tail_ab.sh): tail 38.9-39.0 us at 8 vs 39.7-39.8 at 4, 40.1-40.2 at 6,
 // 40.3-40.4 at 10.  k_gemv_chain32 keeps 4, so two workgroups still fit a CU.
-// The tail (r04, after the fence-free hand-off and the grouped consumer reads): 12-block chunks,
-// six producers on SIMD1-3, the consumer alone on SIMD0, 4 chunks ahead: 34.8-34.9 vs 36.0-36.3
-// us (593.8-594.5 vs 581.4-582.7 tok/s at 248 tokens; 6 chunks ahead 35.6)
+// The tail (r04, after the fence-free hand-off and the grouped consumer reads): 16-block chunks,
+// eight producers on SIMD1-3 (11 waves), the consumer alone on SIMD0, 4 chunks ahead: 33.8-34.2
+// us per tail, 601.2-604.6 tok/s at 248 tokens, against 12-block chunks 35.1 (591.8-592.8) and
+// the 8-block shape with wave 4 producing beside the consumer 36.0-36.3 (581.4-582.7); 3 chunks
+// ahead 34.8-34.9 (profiles/r04_tail_consumer_ab.txt)
 using C2Gemv = C2Shape<8, 4, false>;
-using C2Tail = C2Shape<12, 4, true>;
+using C2Tail = C2Shape<16, 4, true>;
 
 template <class S>
 struct C2Lds {
