@@ -72,7 +72,43 @@ def pmc_traffic_per_launch(kernel: str, path=None, mode="exact"):
     return sum(vals) / len(vals), os.path.relpath(path, ROOT)
 
 
-def roofline_from_profile(kernels, wall_s, mode):
+# The exact path's chain floor: every output row is one sequential fp32 chain of
+# K/2 dependent adds (imax.c:1182-1230), and a dependent v_add_f32 takes 4.63 cycles of the
+# 2.40 GHz clock (tools/chain_lat.hip, profiles/r04_chain_lat.txt).  A launch cannot end before
+# its longest chain has run; chain_floor_frac = that floor / the launch's average time.
+CHAIN_CYCLES_PER_ADD = 4.63
+CHAIN_CLOCK_GHZ = 2.40
+
+
+def chain_adds(kernel: str, E: int, F: int):
+    """Dependent adds of the longest chain in one launch of `kernel` (exact-mode GEMV kernels),
+    or None for kernels without a row chain."""
+    if not kernel.startswith(("k_gemv_solo", "k_gemv_chain32", "k_layer_tail")):
+        return None
+    return (F if "fc_out" in kernel else E) // 2
+
+
+def kernel_stats_file(mode="exact"):
+    """The newest profiles/rNN_<mode>_kernel_stats.csv (rocprofv3 --stats, tools/gpu_round.sh)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{mode}_kernel_stats.csv")))
+    return files[-1] if files else None
+
+
+def rocprof_avg_us(kernel: str, mode="exact"):
+    """(average duration in us of `kernel` in the newest rocprof stats of this mode, its file)."""
+    import csv
+    path = kernel_stats_file(mode)
+    if not path:
+        return None, None
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if f"vsim::{kernel}" in r.get("Name", "") or f"vsim::{kernel}<" in r.get("Name", ""):
+                return float(r["AverageNs"]) / 1e3, os.path.relpath(path, ROOT)
+    return None, os.path.relpath(path, ROOT)
+
+
+def roofline_from_profile(kernels, wall_s, mode, E=None, F=None):
     """The dominant kernel (most device time over the profiled steps): algorithmic bytes per
     launch / its event-timed average launch, against the HBM peak.  The aggregate over every
     profiled launch is kept under a separate key."""
@@ -86,6 +122,16 @@ def roofline_from_profile(kernels, wall_s, mode):
     traffic, src = pmc_traffic_per_launch(rname, mode=mode)
     tot_ms = sum(k["ms"] for k in kernels)
     tot_b = sum(k["bytes"] for k in kernels)
+
+    def floor(k):
+        n = chain_adds(k["name"], E, F) if mode == "exact" and E else None
+        if n is None:
+            return {}
+        fl = n * CHAIN_CYCLES_PER_ADD / (CHAIN_CLOCK_GHZ * 1e3)
+        return {"chain_adds": n, "chain_floor_us": round(fl, 2),
+                "chain_floor_frac": round(fl / (1e3 * k["ms"] / k["launches"]), 4)}
+
+    rp_us, rp_src = rocprof_avg_us(rname, mode)
     return {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
         "frac": round(achieved / PEAK_HBM_GBS, 4),
@@ -93,17 +139,25 @@ def roofline_from_profile(kernels, wall_s, mode):
         "traffic_source": src,
         "kernel": dom["name"], "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_ms * 1e3, 3),
         "launches": dom["launches"],
+        # the same kernel's average from the newest committed rocprofv3 --stats pass (graph replay,
+        # no event pair around each launch), and the frac it gives
+        "rocprof_avg_us": round(rp_us, 3) if rp_us else None,
+        "frac_rocprof": round(bpl / (rp_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4) if rp_us else None,
+        "rocprof_source": rp_src,
+        **floor(dom),
         "per_kernel": [{"kernel": k["name"], "launches": k["launches"],
                         "avg_us": round(1e3 * k["ms"] / k["launches"], 3),
                         "bytes_per_launch": round(k["bytes"] / k["launches"]),
                         "GBps": round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1),
                         "frac": round(k["bytes"] / (k["ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                        "share_of_device_time": round(k["ms"] / tot_ms, 4)} for k in kernels],
+                        "share_of_device_time": round(k["ms"] / tot_ms, 4), **floor(k)} for k in kernels],
         "aggregate": {"GBps": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
                       "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                       "device_share_of_wall": round(tot_ms * 1e-3 / wall_s, 4)},
-        "note": ("exact mode is bound by the reference's sequential fp32 add chain per row "
-                 "(K/2 dependent adds), not by HBM: see DESIGN.md 'chain floor'")
+        "note": ("exact mode: every row is the reference's sequential fp32 chain of K/2 dependent adds; "
+                 "chain_floor_us is that chain alone at 4.63 cycles per add (2.4 GHz), so chain_floor_frac "
+                 "says how far a kernel sits from its own chain bound and frac how far from HBM's "
+                 "(DESIGN.md §4.1; the chain floor of the whole GPT-J-6B token is ~0.56 ms, ~1,800 tok/s)")
         if mode == "exact" else None,
     }
 
@@ -217,16 +271,20 @@ def fast_companion(model, n_past, tok, steps):
     against exact mode (each step is evaluated in both modes from the same exact KV cache;
     over many steps the error compounds through the 4-bit activation re-quantization, see
     tools/mode_drift.py), so it is a reported companion, not the headline value."""
-    rel, agree = [], 0
-    for i in range(4):
+    # (r05: 16 compared steps instead of 4, listed per step: with 4 the agreement moved between
+    # 0.5 and 1.0 with the warm-up length alone -- the driver's --warmup 5 starts the comparison
+    # at position 10, the default 8 at 13 -- on the same kernels, profiles/r05_fast_top1.txt)
+    rel, top1 = [], []
+    ncmp = 16
+    for i in range(ncmp):
         model.set_mode(hip.MODE_FAST)
         lf = model.eval(n_past + i, [tok])
         model.set_mode(hip.MODE_EXACT)
         le = model.eval(n_past + i, [tok])
         rel.append(float(np.max(np.abs(lf - le)) / np.max(np.abs(le))))
-        agree += int(np.argmax(lf) == np.argmax(le))
+        top1.append(int(np.argmax(lf) == np.argmax(le)))
         tok = int(np.argmax(le))
-    n_past += 4
+    n_past += ncmp
     model.set_mode(hip.MODE_FAST)
     toks = model.generate(n_past, tok, 4)  # warm-up (captures the fast-mode graph)
     n_past += 4
@@ -245,8 +303,42 @@ def fast_companion(model, n_past, tok, steps):
             "kernels": ("k_gemv_fast_epi GEMVs beside the exact attention and LayerNorm kernels (serial-residual step)"
                         if model.arch == hip.ARCH_BLOOM else
                         "k_fast_gemv (LayerNorm prologue), k_fast_tail, k_fast_oproj_join (fast_decode.hip)"),
-            "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": agree / len(rel),
+            "one_step_max_rel_logit_err": max(rel), "one_step_top1_agree": sum(top1) / len(top1),
+            "compared_from_position": n_past - ncmp - 4,
+            "per_step_max_rel": [round(r, 5) for r in rel], "per_step_top1": top1,
             "parity": "not bit-exact; drifts across steps (tools/mode_drift.py)"}
+
+
+def decode_companion(config, dev, steps=64, warmup=8):
+    """Exact greedy decode of another BASELINE config on this GPU (BASELINE.json configs[2]:
+    pythia-12b, the HBM-bound GEMV config), bounded: synthetic weights of its shapes, the same
+    5-token prompt, `warmup` then `steps` timed tokens through vsim_model_generate."""
+    import torch
+    arch_s, hp = mg.CONFIGS[config]
+    t0 = time.perf_counter()
+    m = hip.Model.create(ARCHS[arch_s], dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
+                                             n_layer=hp.n_layer, n_rot=hp.n_rot,
+                                             use_parallel_residual=hp.use_parallel_residual),
+                         n_ctx=len(PROMPT) + warmup + steps + 8, device=dev)
+    m.randomize(seed=4321, std=0.02)
+    m.set_mode(hip.MODE_EXACT)
+    m.set_graph(True)
+    tok = int(np.argmax(m.eval(0, PROMPT)))
+    n_past = len(PROMPT)
+    tok = m.generate(n_past, tok, warmup)[-1]
+    n_past += warmup
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    m.generate(n_past, tok, steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t1
+    m.close()
+    bw = q4_weight_bytes(arch_s, hp)
+    return {"value": round(steps / dt, 3), "unit": "tokens/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(1e3 * dt / steps, 4), "mode": "exact",
+            "weight_bytes_per_token": bw, "weight_stream_GBps": round(bw * steps / dt / 1e9, 1),
+            "positions": f"{len(PROMPT) + warmup}..{len(PROMPT) + warmup + steps - 1}",
+            "setup_s": round(t1 - t0, 1)}
 
 
 def run_pipeline(args, world, rank, dev, dist):
@@ -461,6 +553,8 @@ def main():
                     help="gloo: host-staged sends, for rehearsing the pipeline with ranks sharing a GPU")
     ap.add_argument("--no-pipeline-20b", action="store_true",
                     help="skip the GPT-NeoXT-20B layer-split companion measurement")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the bounded pythia-12b exact-decode companion measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -538,7 +632,7 @@ def main():
         prof_wall = time.perf_counter() - t1
         kernels = model.profile_kernels()
         model.set_profile(False)
-        roofline = roofline_from_profile(kernels, prof_wall, args.mode)
+        roofline = roofline_from_profile(kernels, prof_wall, args.mode, hp.n_embd, hp.n_ff)
         if roofline is not None:
             roofline["measured_copy_GBps"] = measured_copy_gbps()
             roofline["frac_of_measured_copy"] = round(roofline["achieved"] / roofline["measured_copy_GBps"], 4)
@@ -575,6 +669,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(arch_s, hp)
     model.close()
+    if rank == 0 and world == 1 and not args.no_other_configs and args.config == "gpt-j-6B" and args.mode == "exact":
+        line["other_configs"] = {"pythia-12b": decode_companion("pythia-12b", dev)}
     if not args.no_pipeline_20b and args.config == "gpt-j-6B":
         if dist is not None:
             dist.barrier()

@@ -46,6 +46,8 @@ extern "C" {
 #define VSIM_ENOMEM (-3)
 #define VSIM_EFILE (-4)
 #define VSIM_ENODEV (-5)
+#define VSIM_ESPIN (-6) /* a bounded cross-workgroup wait inside a fused kernel gave up: the
+                           call's results are not valid (vsim_spin_timeouts counts them)  */
 
 /* numeric modes */
 #define VSIM_MODE_EXACT 0 /* bit-identical to the reference at --threads 1            */
@@ -171,10 +173,12 @@ int vsim_op_get_rows(const void *w, int K, int V, const int32_t *rows, int n, fl
 /* ggml_norm (ggml.c:4246-4304); optional affine y = w*y + b (w, b may be NULL) */
 int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, void *stream);
 /* cumulative counts of exact-LayerNorm rows that needed the sequential fallback:
- * out[0] = mean not certified, out[1] = variance scale not certified (device-wide) */
+ * out[0] = mean not certified, out[1] = variance scale not certified (summed over devices) */
 int vsim_norm_fallbacks(unsigned out[2]);
-/* cumulative count of bounded cross-workgroup waits that gave up (the fused layer tail's wait for
- * its attention heads; placement-independent by construction, so 0 in every healthy run) */
+/* cumulative count of bounded cross-workgroup waits that gave up, summed over devices: the
+ * fused layer tail's wait for its attention heads, the barrier-free chain GEMV's ring hand-off,
+ * the prompt GEMM's stream-K finisher.  0 in every healthy run; the model calls (eval,
+ * eval_argmax, generate, sync) return VSIM_ESPIN when their device's count grew. */
 int vsim_spin_timeouts(unsigned *out);
 int vsim_op_gelu(const float *x, float *y, int n, void *stream);
 /* scale -> diag_mask_inf(n_past) -> soft_max over p[nz][nr][nc], in place */
@@ -185,6 +189,14 @@ int vsim_op_rope(int style, float *x, int d, int H, int T, int n_past, int n_dim
 int vsim_op_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, float *kq,
                void *stream);
 int vsim_op_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, void *stream);
+/* the same with the prompt's causal mask (query j sees keys <= n_past + j, ggml.c:5764-5798):
+ * KQ leaves fully masked 64 x 64 tiles unwritten (diag_mask_inf overwrites them), KQV stops each
+ * query tile's chains at its last unmasked key (every later probability is +0) - the model's
+ * exact prompt path (run_layer) */
+int vsim_op_kq_causal(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, int n_past,
+                      float *kq, void *stream);
+int vsim_op_kqv_causal(const float *V, int ldv, const float *S, int d, int H, int nk, int n, int n_past, float *out,
+                       void *stream);
 /* Fast-mode prompt attention (fp16 MFMA, one pass with an online softmax): for N queries
  * Q [N][d*H] at positions n_past.., keys/values kc/vc [n_past+N][d*H] (post-RoPE K),
  * out[q][h*d + dd] = softmax_k(scale * K.Q, causal) . V.  d in {64, 96, 128, 256}. */

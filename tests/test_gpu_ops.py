@@ -287,6 +287,42 @@ def test_kq_kqv_tiled_vs_oracle(d, H, nk, N):
     assert np.array_equal(bits(host(out)), bits(O.kqv(V, S, d, H, nk, N)))
 
 
+@pytest.mark.parametrize("d,H,N,n_past", [(64, 3, 130, 70), (256, 2, 200, 3), (96, 2, 65, 64), (128, 1, 64, 0)])
+def test_kq_kqv_causal_vs_oracle(d, H, N, n_past):
+    """The causal skipping of the exact prompt products (attn_exact.hip: fully masked KQ tiles left
+    unwritten, KQV chains stopped at the tile's last unmasked key) with multi-tile query batches on
+    top of a cache (n_past > 0) and ragged edges: every unmasked score bit for bit the oracle's,
+    masked ones untouched where a whole tile is masked, and KQV over probabilities that are +0
+    past each query's last key bit for bit the oracle's full chain."""
+    import oracle_py as O
+    nk = n_past + N
+    rng = np.random.default_rng(7 * d + 31 * N + n_past)
+    K = rng.standard_normal((nk, d * H)).astype(np.float32)
+    Q = rng.standard_normal((N, d * H)).astype(np.float32)
+    out = torch.full((H * N * nk,), 12345.0, dtype=torch.float32, device=DEV)
+    Kd, Qd = dev(K), dev(Q)
+    hip.check(hip.lib().vsim_op_kq_causal(Kd.data_ptr(), d * H, Qd.data_ptr(), d * H, d, H, nk, N, n_past,
+                                          out.data_ptr(), None), "kq_causal")
+    got = host(out).reshape(H, N, nk)
+    ref = O.kq(K, Q, d, H, nk, N).reshape(H, N, nk)
+    seen = np.arange(nk)[None, :] <= (n_past + np.arange(N))[:, None]  # query j sees keys <= n_past + j
+    assert np.array_equal(bits(got[:, seen]), bits(ref[:, seen]))
+    # a 64 x 64 tile (query block, key block) whose keys are all past every query's last key
+    for q0 in range(0, N, 64):
+        for k0 in range(0, nk, 64):
+            if k0 > n_past + min(q0 + 64, N) - 1:
+                assert np.all(got[:, q0:q0 + 64, k0:k0 + 64] == 12345.0), (q0, k0)
+    V = rng.standard_normal((nk, d * H)).astype(np.float32)
+    S = rng.random((H, N, nk)).astype(np.float32)
+    S[S < 0.3] = 0.0
+    S[:, ~seen] = 0.0  # what softmax leaves past the mask
+    out = torch.empty(H * N * d, dtype=torch.float32, device=DEV)
+    Vd, Sd = dev(V), dev(S)
+    hip.check(hip.lib().vsim_op_kqv_causal(Vd.data_ptr(), d * H, Sd.data_ptr(), d, H, nk, N, n_past,
+                                           out.data_ptr(), None), "kqv_causal")
+    assert np.array_equal(bits(host(out)), bits(O.kqv(V, S, d, H, nk, N)))
+
+
 def test_get_rows_bit_exact():
     z = ops("getrows")
     K, V = (int(v) for v in z["shape"])

@@ -2,7 +2,11 @@
 groups of G (G reads back to back after every 4G adds; one lgkmcnt wait per group instead of
 one per read), optionally with the tail shape replaced.
 usage: python tools/variants/mk_cons_group.py OUT.hip G ["CB, DEPTH, FILL"]"""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import replace_exact  # noqa: E402
 
 src = open("vsim_amd/csrc/gemv_chain.hip").read()
 g = int(sys.argv[2])
@@ -36,10 +40,8 @@ new = f"""#pragma unroll
         __builtin_amdgcn_sched_group_barrier(0x002, {4 * g}, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, {g}, 0);
       }}"""
-assert src.count(old) == 1
-src = src.replace(old, new)
+src = replace_exact(src, old, new)
 if len(sys.argv) > 3:
     o = "using C2Tail = C2Shape<8, 8, false>;"
-    assert src.count(o) == 1
-    src = src.replace(o, f"using C2Tail = C2Shape<{sys.argv[3]}>;")
+    src = replace_exact(src, o, f"using C2Tail = C2Shape<{sys.argv[3]}>;")
 open(sys.argv[1], "w").write(src)

@@ -3,12 +3,16 @@ ds_read_b128 (lanes 0-31 terms 8i..8i+3 of row lr, lanes 32-63 terms 8i+4..8i+7 
 and brings the upper half-wave's four down with v_permlane32_swap: half the LDS read
 instructions of the consumer, four swaps each (independent of the chain).
 usage: python tools/variants/mk_cons_perm.py OUT.hip G   (G reads per group, 8G adds)"""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import index_or_die  # noqa: E402
 
 src = open("vsim_amd/csrc/gemv_chain.hip").read()
 g = int(sys.argv[2])
-a = src.index("  // --------------------------------------------------------------- consumer (lanes 0-31)")
-b = src.index("  // ----------------------------------------------------------------- epilogue")
+a = index_or_die(src, "  // --------------------------------------------------------------- consumer (lanes 0-31)")
+b = index_or_die(src, "  // ----------------------------------------------------------------- epilogue")
 new = f"""  // --------------------------------------------------------------- consumer (lanes 0-31)
   float acc = 0.0f;
   constexpr int W2 = C2_WIN / 2, NR = CP / 8;  // reads in flight, reads per chunk (8 terms each)

@@ -1,7 +1,11 @@
 """A/B copy of vsim_amd/csrc/gemv_chain.hip whose k_layer_tail out-projection tiles load their
 first NCH chunks of weights (nibbles and scales) once while they wait for the heads, so the LDS-DMA
 after the wait hits L2.  usage: python tools/variants/mk_oproj_prefetch.py OUT.hip NCH"""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import replace_exact  # noqa: E402
 
 src = open("vsim_amd/csrc/gemv_chain.hip").read()
 nch = int(sys.argv[2])
@@ -29,8 +33,7 @@ new = f"""  b -= na;
   }}
   if (threadIdx.x == 0) {{
     unsigned spins = 0;"""
-assert src.count(old) == 1
-src = src.replace(old, new)
+src = replace_exact(src, old, new)
 old2 = """  __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   chain32_body(T.o, b, L.g);"""
@@ -38,6 +41,5 @@ new2 = """  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   chain32_body(T.o, b, L.g);"""
-assert src.count(old2) == 1
-src = src.replace(old2, new2)
+src = replace_exact(src, old2, new2)
 open(sys.argv[1], "w").write(src)

@@ -1,7 +1,11 @@
 """A/B copy of vsim_amd/csrc/gemv_chain.hip whose k_gemv_solo consumer issues its LDS reads in
 groups of G (G reads back to back after every 4G adds), as chain32's consumer does since r04.
 usage: python tools/variants/mk_solo_group.py OUT.hip G [WIN]"""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import replace_exact  # noqa: E402
 
 src = open("vsim_amd/csrc/gemv_chain.hip").read()
 g = int(sys.argv[2])
@@ -35,10 +39,8 @@ new = f"""#pragma unroll
         __builtin_amdgcn_sched_group_barrier(0x002, {4 * g}, 0);  // VALU x{4 * g}
         __builtin_amdgcn_sched_group_barrier(0x100, {g}, 0);  // DS read x{g}
       }}"""
-assert src.count(old) == 1
-src = src.replace(old, new)
+src = replace_exact(src, old, new)
 if len(sys.argv) > 3:
     o = "  static constexpr int WIN = 12;"
-    assert src.count(o) == 1
-    src = src.replace(o, f"  static constexpr int WIN = {sys.argv[3]};")
+    src = replace_exact(src, o, f"  static constexpr int WIN = {sys.argv[3]};")
 open(sys.argv[1], "w").write(src)

@@ -6,6 +6,9 @@ usage: python tools/variants/mk_tail_coherent.py OUTDIR"""
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import replace_exact  # noqa: E402
+
 out = sys.argv[1]
 os.makedirs(out, exist_ok=True)
 g = open("vsim_amd/csrc/gemv_chain.hip").read()
@@ -13,8 +16,7 @@ k = open("vsim_amd/csrc/kern.hpp").read()
 
 
 def rep(s, old, new):
-    assert s.count(old) == 1, old
-    return s.replace(old, new)
+    return replace_exact(s, old, new)
 
 
 k = rep(k, "__device__ __forceinline__ void glds4(const void *g, uint32_t lds) {", """__device__ __forceinline__ void glds16_sc1(const void *g, uint32_t lds) {

@@ -7,15 +7,18 @@ tools/build_variant.sh stamps gemv_chain.hip =OUT.hip.  Stamps per tile and step
  [3..6] producer wave 1 (p = 0): top, after the pair terms and stores, after its vmcnt wait,
  after the barrier; [7..10] the same for p = 2 (wave 3); [11] s_memrealtime
  at the consumer's step top (100 MHz)."""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import replace_exact  # noqa: E402
 
 src = open("vsim_amd/csrc/gemv_chain.hip").read()
 
 
 def rep(old, new, count=1):
     global src
-    assert src.count(old) >= count, old
-    src = src.replace(old, new, count)
+    src = replace_exact(src, old, new, count)
 
 
 rep("""__device__ __forceinline__ void producer_barrier()""",

@@ -8,6 +8,9 @@ gemv_chain.hip =OUTDIR/gemv_chain.hip attn.hpp =OUTDIR/attn.hpp)"""
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from anchor import replace_exact  # noqa: E402
+
 out = sys.argv[1]
 os.makedirs(out, exist_ok=True)
 g = open("vsim_amd/csrc/gemv_chain.hip").read()
@@ -15,8 +18,7 @@ a = open("vsim_amd/csrc/attn.hpp").read()
 
 
 def rep(s, old, new):
-    assert s.count(old) == 1, old
-    return s.replace(old, new)
+    return replace_exact(s, old, new)
 
 
 a = rep(a, "namespace vsim {\n", """namespace vsim {

@@ -64,6 +64,10 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   }
   __syncthreads();
   for (int i = tid; i < d; i += ATT_THREADS) A.kc[(size_t)n_past * E + h * d + i] = kh[i];
+  // The new key's row is read back below by whichever wave holds key n_past (wave n_past/16 %
+  // waves), not only by the threads that stored it: the barrier (its release drains the stores)
+  // orders them.  r05: until then that read raced the store whenever n_past >= 16.
+  __syncthreads();
   // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale.
   // Row r (lanes 16r..16r+15) of a wave takes one key per step; lane l16 covers the float4s
   // at 4*l16 + 64*e of the head dimension.  A wave loads ATT_KB steps (4*ATT_KB keys) at once.

@@ -185,8 +185,6 @@ __global__ void __launch_bounds__(AP_THREADS) k_attn_prefill_f16(const float *__
           const int krow = 32 * t + r;
           const ahalf8 kf = *(const ahalf8 *)&Ks[krow * KLD + 16 * s + 8 * hl];
           st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], st[t], 0, 0, 0);
-          // (a scheduling fence every 4 steps: the compiler would otherwise hoist all the
-          // tile's LDS reads and run out of registers at D = 256)
         }
       }
     }

@@ -144,6 +144,16 @@ int vsim_op_kq(const float *K, int ldk, const float *Q, int ldq, int d, int H, i
 int vsim_op_kqv(const float *V, int ldv, const float *S, int d, int H, int nk, int n, float *out, void *stream) {
   return launch_kqv(V, ldv, S, d, H, nk, n, out, 0, (hipStream_t)stream);
 }
+int vsim_op_kq_causal(const float *K, int ldk, const float *Q, int ldq, int d, int H, int nk, int n, int n_past,
+                      float *kq, void *stream) {
+  if (n_past < 0) { set_error("kq_causal: n_past must be >= 0"); return VSIM_EINVAL; }
+  return launch_kq(K, ldk, Q, ldq, d, H, nk, n, kq, (hipStream_t)stream, n_past);
+}
+int vsim_op_kqv_causal(const float *V, int ldv, const float *S, int d, int H, int nk, int n, int n_past, float *out,
+                       void *stream) {
+  if (n_past < 0) { set_error("kqv_causal: n_past must be >= 0"); return VSIM_EINVAL; }
+  return launch_kqv(V, ldv, S, d, H, nk, n, out, 0, (hipStream_t)stream, n_past);
+}
 int vsim_op_attn_prefill(const float *Q, const float *kc, const float *vc, int d, int H, int N, int n_past,
                          float scale, float *out, void *stream) {
   return launch_attn_prefill_f16(Q, kc, vc, d, H, N, n_past, scale, out, (hipStream_t)stream);

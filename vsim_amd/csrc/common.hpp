@@ -250,10 +250,14 @@ struct DevTables {
   const uint16_t *exp_f16;   // table_exp_f16 (ggml.c:1249)
   const uint16_t *gelu_f16;  // table_gelu_f16 (ggml.c:1247)
 };
-int tables_get(DevTables *t);
-int norm_stats(unsigned *out2);
-unsigned *spin_error_counter();  // device counter of bounded waits that gave up (null before tables_get)
-int spin_timeouts(unsigned *out);  // LayerNorm fallback counters (ops_elt.hip)  // lazily uploads host-built tables for the current device
+int tables_get(DevTables *t);  // lazily uploads host-built tables for the current device
+// Health counters of the current device (ops_elt.hip; null before tables_get on that device):
+// LayerNorm fallbacks, and the bounded cross-workgroup waits that gave up
+unsigned *dev_stats();
+unsigned *spin_error_counter();
+int norm_stats(unsigned *out2);              // LayerNorm fallbacks, summed over devices
+int spin_timeouts(unsigned *out);            // waits that gave up, summed over devices
+int spin_timeouts_dev(int dev, unsigned *out);
 
 int launch_q4_repack(const void *aos, void *soa, int rows, int k, hipStream_t s);
 int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s);

@@ -681,8 +681,14 @@ constexpr int r_lds_bytes() { return 2 * 4 * G2_PIECE * 2; }
 // checks no tile has 3 pieces and sizes the grid to the device's CUs (at most one workgroup per
 // CU is needed for all of them to be resident at once).  The publisher publishes before it waits
 // on anything, so whatever order the workgroups are dispatched in, a waiter's publisher runs as
-// soon as it has a CU; the wait is bounded all the same (SK_SPIN_MAX sleeps, ~1 s: past it the
-// error counter vsim_spin_timeouts is bumped).  r04 tried a wait-free variant (the second of
+// soon as it has a CU.  Liveness therefore needs every workgroup of the grid resident at once:
+// with the XCD remap (xcd_index, r04) a tile's publisher can have a HIGHER blockIdx than its
+// finisher, so "waits only on lower-indexed, already dispatched workgroups" no longer holds, and
+// the grid (hipDeviceAttributeMultiprocessorCount workgroups, one per CU by launch bounds and LDS)
+// relies on the whole device being available to this process.  On a CU-masked or shared device a
+// finisher can wait on an undispatched publisher; the wait is bounded (SK_SPIN_MAX sleeps, ~1 s),
+// past it the per-device error counter (vsim_spin_timeouts) is bumped and the model call that
+// ran the prompt fails with VSIM_ESPIN.  r04 tried a wait-free variant (the second of
 // the two pieces to arrive finishes the tile, from an atomic counter): with two epilogue sites
 // the kernel spilled 100-350 VGPRs (scratch traffic beside the counted vmcnt waits) and ran
 // 0.5 ms slower per codegen-16B prompt (61.7 vs 61.1-61.2 ms); not kept.

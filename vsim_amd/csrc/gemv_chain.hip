@@ -264,6 +264,218 @@ __global__ void __launch_bounds__(C2Gemv::THREADS, 2) k_gemv_chain32(GemvBatch B
   chain32_body(B, blockIdx.x, L);
 }
 
+// ================================================================== 32-row, barrier-free
+// The same chains and pair terms as chain32_body with no workgroup barrier in the loop: the
+// consumer and each producer hand the pair-term ring over through LDS counters instead.
+//  * ready[s]: producers add 1 after their terms of a chunk in slot s landed (lgkmcnt(0));
+//    chunk c is complete when ready[c % NB_RING] reaches NPW * (c / NB_RING + 1);
+//  * cons: chunks the consumer has read into registers; a producer writes chunk k into its slot
+//    once cons >= k - NB_RING + 1.
+// Each producer brings its own weights, scales and activation factors by LDS-DMA (DEPTH chunks
+// ahead, retired by its own counted vmcnt), so no wave waits for another's loads.  The consumer
+// reads its 256 pair terms per chunk in batches of 8 16-byte reads issued one batch ahead of the
+// 32 adds they feed; the next chunk's ready count is read with the last batch.  Why: the
+// barrier version's per-chunk s_barrier and lgkmcnt(0) drain cost the chain 8.5 cycles per add
+// against the 4.3 the batched loop reaches alone (profiles/r04_cons_lat3.txt).
+// The 32 chain adds of one consumer batch (8 float4 in registers) as ONE volatile asm statement
+// with a memory clobber: the compiler keeps each batch's LDS reads in front of the adds they
+// overlap (left to itself it issued all of a chunk's reads first and spilled them), waits only for
+// the batch being added, and puts no s_nop between statements (it does between separate ones).
+#define NB_A4(i) "v_add_f32 %0, %0, %" #i "\n\t"
+#define NB_BATCH_ADDS(acc, cur)                                                                                 \
+  asm volatile(NB_A4(1) NB_A4(2) NB_A4(3) NB_A4(4) NB_A4(5) NB_A4(6) NB_A4(7) NB_A4(8) NB_A4(9) NB_A4(10) NB_A4(11) \
+                   NB_A4(12) NB_A4(13) NB_A4(14) NB_A4(15) NB_A4(16) NB_A4(17) NB_A4(18) NB_A4(19) NB_A4(20)      \
+                       NB_A4(21) NB_A4(22) NB_A4(23) NB_A4(24) NB_A4(25) NB_A4(26) NB_A4(27) NB_A4(28) NB_A4(29)  \
+                           NB_A4(30) NB_A4(31) NB_A4(32)                                                         \
+               : "+v"(acc)                                                                                       \
+               : "v"(cur[0].x), "v"(cur[0].y), "v"(cur[0].z), "v"(cur[0].w), "v"(cur[1].x), "v"(cur[1].y),       \
+                 "v"(cur[1].z), "v"(cur[1].w), "v"(cur[2].x), "v"(cur[2].y), "v"(cur[2].z), "v"(cur[2].w),       \
+                 "v"(cur[3].x), "v"(cur[3].y), "v"(cur[3].z), "v"(cur[3].w), "v"(cur[4].x), "v"(cur[4].y),       \
+                 "v"(cur[4].z), "v"(cur[4].w), "v"(cur[5].x), "v"(cur[5].y), "v"(cur[5].z), "v"(cur[5].w),       \
+                 "v"(cur[6].x), "v"(cur[6].y), "v"(cur[6].z), "v"(cur[6].w), "v"(cur[7].x), "v"(cur[7].y),       \
+                 "v"(cur[7].z), "v"(cur[7].w)                                                                    \
+               : "memory");                                                                                      \
+  _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) cur[j_] = nxt[j_]
+constexpr int NB_RING = 3;
+constexpr unsigned NB_SPIN_MAX = 1u << 24;
+template <class S>
+struct NbLds {
+  float P[NB_RING][32 * S::LD];
+  uint4 RQ[S::DEPTH][S::NPW][64];
+  float RD[S::DEPTH][S::NPW][64];
+  float RX[S::DEPTH][S::NPW][64];
+  unsigned ready[NB_RING];
+  unsigned cons;
+};
+
+__device__ __forceinline__ unsigned lds_load(const unsigned *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// SC1: the activation factors were written write-through by other workgroups of this launch
+template <class S, bool SC1>
+__device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err) {
+  constexpr int DEPTH = S::DEPTH, CB = S::CB, LD = S::LD, NPW = S::NPW;
+  constexpr int WAIT_VM = waitcnt_vm(3 * (DEPTH - 1));  // chunk c landed, c+1 .. c+DEPTH-1 in flight
+  static_assert(3 * (DEPTH - 1) < 64, "vmcnt immediate");
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  int ji = 0;
+  while (ji < B.nj) {
+    if (t < B.j[ji].w.tiles) break;
+    t -= B.j[ji].w.tiles;
+    ++ji;
+  }
+  if (ji >= B.nj) return;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const int nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
+  if (threadIdx.x < NB_RING) L.ready[threadIdx.x] = 0;
+  if (threadIdx.x == 0) L.cons = 0;
+  __syncthreads();
+  if (S::FILL && wave > 0 && wave % 4 == 0) return;  // the consumer's SIMD is left to it
+
+  if (wave > 0) {
+    // ------------------------------------------------------------- producer
+    const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
+    const int o = 2 * p + hb;  // this lane's block within the chunk
+    const uint8_t *qs = B.j[ji].w.qs + (size_t)t * nb * T32 * 16 + (size_t)r * 16;
+    const float *dd = B.j[ji].w.d + (size_t)t * nb * T32 + r;
+    const float *xr = B.j[ji].xd + r;
+    // every chunk up to nch + DEPTH is loaded (block clamped), so the counted waits hold
+    auto dma = [&](int c) {
+      const int slot = c % DEPTH;
+      const int b = min(c * CB + o, nb - 1);
+      glds16(qs + (size_t)b * (T32 * 16), lds_addr(&L.RQ[slot][p][0]));
+      glds4(dd + (size_t)b * T32, lds_addr(&L.RD[slot][p][0]));
+      if constexpr (SC1)
+        glds4_sc1(xr + (size_t)b * QK, lds_addr(&L.RX[slot][p][0]));
+      else
+        glds4<false>(xr + (size_t)b * QK, lds_addr(&L.RX[slot][p][0]));
+    };
+    auto ldraw = [&](int c, uint4 &q, float &dq, f32x2 *xv) {
+      const int slot = c % DEPTH;
+      __builtin_amdgcn_s_waitcnt(WAIT_VM);
+      q = L.RQ[slot][p][lane];
+      dq = L.RD[slot][p][lane];
+      const float4 *xq = (const float4 *)&L.RX[slot][p][hb * 32];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 v = xq[i];
+        xv[2 * i].x = v.x;
+        xv[2 * i].y = v.y;
+        xv[2 * i + 1].x = v.z;
+        xv[2 * i + 1].y = v.w;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the slot is reloaded
+      dma(c + DEPTH);
+    };
+    auto compute = [&](int k, const f32x2 *xc, const uint4 &qc, float dqc) {
+      const int slot = k % NB_RING;
+      if (k >= NB_RING) {
+        unsigned spins = 0;
+        while ((int)lds_load(&L.cons) < k - NB_RING + 1) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins == NB_SPIN_MAX) {
+            if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        asm volatile("" ::: "memory");
+      }
+      const float dv = k * CB + o < nb ? dqc : 0.0f;
+      const f32x2 d2 = {512.0f * dv, 512.0f * dv}, m2 = {-8.0f * dv, -8.0f * dv};
+      float *dst = &L.P[slot][r * LD + o * 16];
+      const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) {
+        float p4[4];
+        pair_terms4_x(qw[wv], d2, m2, xc + 4 * wv, p4);
+        *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the terms are in LDS before the count
+      if (lane == 0) __hip_atomic_fetch_add(&L.ready[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#pragma unroll
+    for (int c = 0; c < DEPTH; ++c) dma(c);
+    f32x2 xa[16], xb[16];
+    uint4 qa, qb;
+    float da, db;
+    ldraw(0, qa, da, xa);
+    for (int k = 0; k < nch; k += 2) {
+      ldraw(k + 1, qb, db, xb);
+      compute(k, xa, qa, da);
+      ldraw(k + 2, qa, da, xa);
+      if (k + 1 < nch) compute(k + 1, xb, qb, db);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
+    return;
+  }
+
+  // --------------------------------------------------------------- consumer (lanes 0-31)
+  float acc = 0.0f;
+  const int lr = lane & 31;
+  constexpr int NV = S::CP / 4, BQ = 8, NBQ = NV / BQ;  // float4 per chunk, per batch, batches
+  static_assert(NV % BQ == 0 && NBQ >= 2, "batches tile the chunk");
+  auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
+  auto wait_ready = [&](int c, unsigned have) {
+    unsigned spins = 0;
+    while (have < need(c)) {
+      have = lds_load(&L.ready[c % NB_RING]);
+      if (++spins == NB_SPIN_MAX) {
+        if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    asm volatile("" ::: "memory");
+  };
+  __builtin_amdgcn_s_setprio(3);
+  wait_ready(0, 0u);
+  f32x4 cur[BQ], nxt[BQ];
+  {
+    const f32x4 *p0 = (const f32x4 *)&L.P[0][lr * LD];
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) cur[j] = p0[j];
+  }
+  static_assert(BQ == 8, "NB_BATCH_ADDS adds 8 float4");
+  auto adds = [&]() { NB_BATCH_ADDS(acc, cur); };
+  for (int c = 0; c < nch; ++c) {
+    const f32x4 *pc = (const f32x4 *)&L.P[c % NB_RING][lr * LD];
+    unsigned rdy = 0;
+#pragma unroll
+    for (int q = 0; q < NBQ - 1; ++q) {
+#pragma unroll
+      for (int j = 0; j < BQ; ++j) nxt[j] = pc[(q + 1) * BQ + j];
+      if (q == NBQ - 2) rdy = lds_load(&L.ready[(c + 1) % NB_RING]);  // (past the last chunk: unused)
+      adds();
+    }
+    // the chunk's last batch is in registers: its slot may be refilled
+    __hip_atomic_store(&L.cons, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (c + 1 < nch) wait_ready(c + 1, rdy);
+    const f32x4 *pn = (const f32x4 *)&L.P[(c + 1) % NB_RING][lr * LD];  // (past the last chunk: harmless)
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) nxt[j] = pn[j];
+    adds();
+  }
+  __builtin_amdgcn_s_setprio(0);
+
+  // ----------------------------------------------------------------- epilogue
+  const int row = t * T32 + lr;
+  const int rows = B.j[ji].w.rows;
+  const float *bias = B.j[ji].bias;
+  float *y = B.j[ji].y;
+  if (B.j[ji].epi == EPI_GELU_Q) {
+    const bool ok = lane < 32 && row < rows;
+    float g = 0.0f;
+    if (ok) {
+      g = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      if (y) y[row] = g;
+    }
+    quantize_half(g, lane, ok, B.j[ji].oq_qs + (size_t)t * 16, B.j[ji].oq_d + t, B.j[ji].oxd + (size_t)t * QK);
+  } else if (lane < 32 && row < rows) {
+    y[row] = bias ? acc + bias[row] : acc;
+  }
+}
+
 // ================================================================== fused layer tail
 // fc_out, the attention heads and the out-projection of one layer in one launch, so the
 // attention and the out-projection run beside fc_out, whose K = 4E chain is the layer's
@@ -295,14 +507,19 @@ struct TailJob {
   int nf;
 };
 
+template <int NBM>
 __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   __shared__ union {
     C2Lds<C2Tail> g;
+    NbLds<C2Tail> n;
     float a[sizeof(C2Lds<C2Tail>) / sizeof(float)];
   } L;
   int b = blockIdx.x;
   if (b < T.nf) {
-    chain32_body(T.f, b, L.g);
+    if constexpr (NBM & 1)
+      chain32_nb_body<C2Tail, false>(T.f, b, L.n, T.err);
+    else
+      chain32_body(T.f, b, L.g);
     return;
   }
   b -= T.nf;
@@ -326,7 +543,10 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
     }
   }
   __syncthreads();
-  chain32_body(T.o, b, L.g);
+  if constexpr (NBM & 2)
+    chain32_nb_body<C2Tail, true>(T.o, b, L.n, T.err);
+  else
+    chain32_body(T.o, b, L.g);
 }
 
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
@@ -350,7 +570,15 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   // one workgroup per CU (fc_out's consumer keeps its SIMD): the static LDS is above half the
   // CU's already at DEPTH 8, the dynamic pad keeps it so at any depth; the workgroups that find
   // no CU start as attention heads end
-  hipLaunchKernelGGL(k_layer_tail, dim3(T.nf + a.H * S + no), dim3(C2Tail::THREADS), 8192, s, T);
+  static const int nbm = [] {
+    const char *e = getenv("VSIM_TAIL_NB");
+    return e ? atoi(e) & 3 : 0;
+  }();
+  const dim3 grid(T.nf + a.H * S + no), blk(C2Tail::THREADS);
+  if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, 8192, s, T);
+  if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, 8192, s, T);
+  if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, 8192, s, T);
+  if (nbm == 3) hipLaunchKernelGGL(k_layer_tail<3>, grid, blk, 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -541,6 +769,187 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   __builtin_amdgcn_s_setprio(0);
 }
 
+// ---------------------------------------------------------------- 64-row, barrier-free
+// k_gemv_solo's shape and arithmetic with the chain32_nb_body hand-off in place of the per-chunk
+// barrier: each producer counts its block of chunk k into ready[k % NB_RING] once its stores
+// landed (at the top of step k+1, whose lgkmcnt(0) also covers its scalar-loaded factors), and
+// waits for the consumer's count before overwriting a slot; the consumer reads in batches of 8.
+// r02's barrier-free variant (per-slot counters too) lost to the barrier with the one-read-per-4-
+// adds consumer; r05 measures it again with the batched consumer.
+template <int CB, int PF>
+__device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*P)[64 * SoloShape<CB, 1>::LD],
+                                             unsigned *ready, unsigned *consw, unsigned *err) {
+  using S = SoloShape<CB, 1>;
+  constexpr int LD = S::LD;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  int ji = 0;
+  while (ji < B.nj) {
+    const int ng = (B.j[ji].w.tiles + 1) / 2;
+    if (g < ng) break;
+    g -= ng;
+    ++ji;
+  }
+  if (ji >= B.nj) return;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  g = __builtin_amdgcn_readfirstlane(g);
+  const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
+  if (threadIdx.x < NB_RING) ready[threadIdx.x] = 0;
+  if (threadIdx.x == 0) *consw = 0;
+  __syncthreads();
+  if ((wave & 3) == 0 && wave > 0) return;  // the consumer's SIMD is left to it
+
+  if (wave != 0) {
+    // ------------------------------------------------------------- producer
+    const int o = wave - 1 - (wave >> 2);  // block of the chunk: waves 1,2,3,5,6,7 -> 0..5
+    const int h = lane >> 5, r = lane & 31;
+    const int tile = 2 * g + h;
+    const bool tile_ok = tile < tiles;
+    const int tl = tile_ok ? tile : tiles - 1;
+    const uint8_t *qs = B.j[ji].w.qs + ((size_t)tl * nb * T32 + r) * 16;
+    const float *dd = B.j[ji].w.d + (size_t)tl * nb * T32 + r;
+    const float *xg = B.j[ji].xd;
+    auto ld = [&](int c, u32x4 &qv, float &dv) {
+      const int b = min(c * CB + o, nb - 1);
+      qv = __builtin_nontemporal_load((gu32x4 *)(qs + (size_t)b * (T32 * 16)));
+      dv = __builtin_nontemporal_load((gfloat *)(dd + (size_t)b * T32));
+    };
+    auto ldx = [&](int c, f32x2 *xv) {
+      const int b = min(c * CB + o, nb - 1);
+      const sfloat *xp = (const sfloat *)(xg + (size_t)b * QK);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        xv[i].x = xp[2 * i];
+        xv[i].y = xp[2 * i + 1];
+      }
+    };
+    auto signal = [&](int c) {  // chunk c's terms are in LDS (after an lgkmcnt(0))
+      if (lane == 0) __hip_atomic_fetch_add(&ready[c % NB_RING], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
+      ld(k + PF, qn, dqn);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this chunk's factors, the last chunk's stores
+      __builtin_amdgcn_sched_barrier(0);
+      if (k > 0) signal(k - 1);
+      ldx(k + 1, xn);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k >= NB_RING) {  // slot k % NB_RING: the consumer is done with chunk k - NB_RING
+        unsigned spins = 0;
+        while ((int)lds_load(consw) < k - NB_RING + 1) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins == NB_SPIN_MAX) {
+            if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        asm volatile("" ::: "memory");
+      }
+      const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
+      const float dl = 512.0f * dv, ml = -8.0f * dv;
+      float dh, mh;
+      asm("v_mov_b32 %0, %1" : "=v"(dh) : "v"(dl));  // (as in solo_body)
+      asm("v_mov_b32 %0, %1" : "=v"(mh) : "v"(ml));
+      const f32x2 d2 = {dl, dh}, m2 = {ml, mh};
+      float *dst = &P[k % NB_RING][lane * LD + o * 16];
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) {
+        float p4[4];
+        pair_terms4_x(qc[wv], d2, m2, xc + 4 * wv, p4);
+        *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    u32x4 q[PF + 1];
+    float e[PF + 1];
+#pragma unroll
+    for (int c = 0; c < PF; ++c) ld(c, q[c], e[c]);
+    f32x2 xa[16], xb[16];
+    ldx(0, xa);
+    static_assert((PF + 1) % 2 == 0, "two factor sets alternate");
+    for (int k = 0; k < nch; k += PF + 1) {
+#pragma unroll
+      for (int u = 0; u < PF + 1; u += 2) {
+        if (k + u < nch) step(k + u, xa, xb, q[u], e[u], q[(u + PF) % (PF + 1)], e[(u + PF) % (PF + 1)]);
+        if (k + u + 1 < nch) step(k + u + 1, xb, xa, q[u + 1], e[u + 1], q[u % (PF + 1)], e[u % (PF + 1)]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    signal(nch - 1);
+    return;
+  }
+
+  // --------------------------------------------------------------- consumer (64 rows)
+  float acc = 0.0f;
+  constexpr int NV = S::CP / 4, BQ = 8, NBQ = NV / BQ, NPW = CB;
+  static_assert(NV % BQ == 0 && NBQ >= 2, "batches tile the chunk");
+  auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
+  auto wait_ready = [&](int c, unsigned have) {
+    unsigned spins = 0;
+    while (have < need(c)) {
+      have = lds_load(&ready[c % NB_RING]);
+      if (++spins == NB_SPIN_MAX) {
+        if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    asm volatile("" ::: "memory");
+  };
+  __builtin_amdgcn_s_setprio(3);
+  wait_ready(0, 0u);
+  f32x4 cur[BQ], nxt[BQ];
+  {
+    const f32x4 *p0 = (const f32x4 *)&P[0][lane * LD];
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) cur[j] = p0[j];
+  }
+  static_assert(BQ == 8, "NB_BATCH_ADDS adds 8 float4");
+  auto adds = [&]() { NB_BATCH_ADDS(acc, cur); };
+  for (int c = 0; c < nch; ++c) {
+    const f32x4 *pc = (const f32x4 *)&P[c % NB_RING][lane * LD];
+    unsigned rdy = 0;
+#pragma unroll
+    for (int q = 0; q < NBQ - 1; ++q) {
+#pragma unroll
+      for (int j = 0; j < BQ; ++j) nxt[j] = pc[(q + 1) * BQ + j];
+      if (q == NBQ - 2) rdy = lds_load(&ready[(c + 1) % NB_RING]);
+      adds();
+    }
+    __hip_atomic_store(consw, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (c + 1 < nch) wait_ready(c + 1, rdy);
+    const f32x4 *pn = (const f32x4 *)&P[(c + 1) % NB_RING][lane * LD];
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) nxt[j] = pn[j];
+    adds();
+  }
+
+  // ----------------------------------------------------------------- epilogue
+  const int row = g * S::ROWS + lane;
+  const int rows = B.j[ji].w.rows;
+  const float *bias = B.j[ji].bias;
+  float *y = B.j[ji].y;
+  if (B.j[ji].epi == EPI_GELU_Q) {
+    const bool ok = row < rows;
+    float gv = 0.0f;
+    if (ok) {
+      gv = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      if (y) y[row] = gv;
+    }
+    const int blk = row / QK;
+    quantize_half(gv, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
+                  B.j[ji].oxd + (size_t)blk * QK);
+  } else if (row < rows) {
+    y[row] = bias ? acc + bias[row] : acc;
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int CB, int PF>
+__global__ void __launch_bounds__((64 * SoloShape<CB, 1>::WAVES), 1) k_gemv_solo_nb(GemvBatch B, unsigned *err) {
+  __shared__ __attribute__((aligned(16))) float P[NB_RING][64 * SoloShape<CB, 1>::LD];
+  __shared__ unsigned ready[NB_RING], consw;
+  solo_nb_body<CB, PF>(B, blockIdx.x, P, ready, &consw, err);
+}
+
 template <int CB, int PF, int CONS>
 __global__ void __launch_bounds__((64 * SoloShape<CB, CONS>::WAVES), 1) k_gemv_solo(GemvBatch B) {
   __shared__ __attribute__((aligned(16))) float P[C5_RING][SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD];
@@ -572,7 +981,14 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     tiles += B.j[i].w.tiles;
   }
   if (tiles == 0) return VSIM_OK;
-  if (gemv_chain_solo(B)) {
+  static const bool solo_nb = [] {
+    const char *e = getenv("VSIM_SOLO_NB");
+    return e && atoi(e) != 0;
+  }();
+  if (gemv_chain_solo(B) && solo_nb) {
+    hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF>), dim3(solo_groups(B)),
+                       dim3(64 * SoloShape<SOLO_CB, 1>::WAVES), 0, s, B, spin_error_counter());
+  } else if (gemv_chain_solo(B)) {
     hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)), dim3(64 * SoloShape<SOLO_CB, 1>::WAVES),
                        0, s, B);
   } else {

@@ -23,8 +23,6 @@
 
 namespace vsim {
 
-extern unsigned *g_norm_stats;
-
 // ------------------------------------------------------------------ 1. LN + quantize
 // One 1024-thread workgroup per LayerNorm (two for GPT-NeoX's parallel-residual pair); the
 // normalized row is quantized by whole waves, two 32-blocks per wave step.
@@ -46,7 +44,7 @@ __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuant
 
 int launch_ln_quant(const LnQuantJob &j0, const LnQuantJob *j1, int n, hipStream_t s) {
   const dim3 grid((j1 ? 2 : 1) * LNQ_SPLIT);
-  hipLaunchKernelGGL(k_ln_quant, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n, g_norm_stats);
+  hipLaunchKernelGGL(k_ln_quant, grid, dim3(LNQ_THREADS), (size_t)n * 4, s, j0, j1 ? *j1 : j0, n, dev_stats());
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

@@ -46,6 +46,7 @@ struct LayerW {
 
 struct vsim_model {
   int arch = VSIM_ARCH_GPTNEOX;
+  unsigned spin_seen = 0;  // the device's spin-timeout count at the last check (spin_check)
   vsim_hparams hp{};
   int n_ctx = 512, device = 0, l0 = 0, l1 = 0;
   bool first = true, last = true;
@@ -441,6 +442,23 @@ void bind_pointers(vsim_model *m) {
     int rc_ = (x);               \
     if (rc_) return rc_;         \
   } while (0)
+
+// After a call's work has been synchronized: a bounded cross-workgroup wait on this device that
+// gave up since the last check (k_layer_tail, the barrier-free chain GEMV, the stream-K
+// finisher) means some tile went on with incomplete data, so the call fails with VSIM_ESPIN
+// instead of returning results that are not the reference's.
+int spin_check(vsim_model *m) {
+  unsigned n = 0;
+  RC(spin_timeouts_dev(m->device, &n));
+  if (n > m->spin_seen) {
+    const unsigned grew = n - m->spin_seen;
+    m->spin_seen = n;
+    set_error("a bounded cross-workgroup wait gave up " + std::to_string(grew) +
+              " time(s) in this call (device " + std::to_string(m->device) + "): results not valid");
+    return VSIM_ESPIN;
+  }
+  return VSIM_OK;
+}
 
 // Profiling brackets (eager launches only): prof_begin records the start event and returns
 // its slot (-1 when profiling is off); prof_end records the end and tags the pair.
@@ -1233,6 +1251,7 @@ int model_create_impl(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   }
   DevTables t;
   if (int rc = tables_get(&t)) return fail(rc);
+  if (int rc = spin_timeouts_dev(m->device, &m->spin_seen)) return fail(rc);  // earlier calls' count
   if (int rc = ensure_scratch(m, 16)) return fail(rc);
   *out = m;
   return VSIM_OK;
@@ -1617,6 +1636,7 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
     m->kernels_last = nk + 1;
   }
   VSIM_HIP(hipStreamSynchronize(s));
+  RC(spin_check(m));
   *next_token = m->am_host[0];
   if (m->profile) RC(prof_collect(m));
   return VSIM_OK;
@@ -1654,6 +1674,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   }
   VSIM_HIP(hipMemcpyAsync(tokens_out, m->hist_dev + n_past, sizeof(int32_t) * n_steps, hipMemcpyDeviceToHost, s));
   VSIM_HIP(hipStreamSynchronize(s));
+  RC(spin_check(m));
   if (m->profile) RC(prof_collect(m));
   return VSIM_OK;
 }
@@ -1747,6 +1768,7 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
     }
   }
   VSIM_HIP(hipStreamSynchronize(s));
+  RC(spin_check(m));
   if (m->last && logits) memcpy(logits, m->logit_host, sizeof(float) * V);
   m->kernels_last = nk;
   if (m->profile) RC(prof_collect(m));
@@ -1807,9 +1829,10 @@ int vsim_model_stage_step(vsim_model *m) {
   m->st_npast++;
   if (m->profile) {
     VSIM_HIP(hipStreamSynchronize(m->stream));
+    RC(spin_check(m));
     RC(prof_collect(m));
   }
-  return VSIM_OK;
+  return VSIM_OK;  // (steps run asynchronously: vsim_model_sync checks them)
 }
 
 int vsim_model_debug_poison(vsim_model *m, int n_tokens) {
@@ -1844,7 +1867,7 @@ int vsim_model_sync(vsim_model *m) {
   if (!m) { set_error("sync: null model"); return VSIM_EINVAL; }
   VSIM_HIP(hipSetDevice(m->device));
   VSIM_HIP(hipStreamSynchronize(m->stream));
-  return VSIM_OK;
+  return spin_check(m);
 }
 
 int vsim_model_set_profile(vsim_model *m, int enable) {

@@ -54,13 +54,22 @@ __global__ void __launch_bounds__(NORMQ_THREADS) k_norm_f16q(const float *__rest
   }
 }
 
-unsigned *g_norm_stats = nullptr;  // device counters of LayerNorm fallbacks (ln_exact_lds)
+// Per-device health counters, allocated with the device's tables (tables_get): [0] LayerNorm
+// mean fallbacks, [1] variance fallbacks (ln_exact_lds), [2] bounded cross-workgroup waits that
+// gave up (k_layer_tail, the stream-K finisher, the barrier-free chain GEMV).  A kernel gets the
+// counters of the device it runs on.
+static unsigned *g_dev_stats[64];
+static int current_device() {
+  int dev = 0;
+  return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 ? dev : 0;
+}
+unsigned *dev_stats() { return g_dev_stats[current_device()]; }
 
 int launch_norm(const float *x, float *y, int k, int rows, const float *w, const float *b, hipStream_t s) {
   if (k <= 0 || rows <= 0) { set_error("norm: bad shape"); return VSIM_EINVAL; }
   if ((w == nullptr) != (b == nullptr)) { set_error("norm: affine needs both w and b"); return VSIM_EINVAL; }
   if ((size_t)k * 4 > 64 * 1024) { set_error("norm: row longer than 16384"); return VSIM_EINVAL; }
-  hipLaunchKernelGGL(k_norm_exact, dim3(rows), dim3(NORM_THREADS), (size_t)k * 4, s, x, y, k, w, b, g_norm_stats);
+  hipLaunchKernelGGL(k_norm_exact, dim3(rows), dim3(NORM_THREADS), (size_t)k * 4, s, x, y, k, w, b, dev_stats());
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -69,7 +78,7 @@ int launch_norm_f16q(const float *x, void *x16, int k, int rows, const float *w,
   if (k <= 0 || rows <= 0 || k % QK || !w || !b) { set_error("norm_f16q: bad shape"); return VSIM_EINVAL; }
   if ((size_t)k * 4 > 64 * 1024) { set_error("norm: row longer than 16384"); return VSIM_EINVAL; }
   hipLaunchKernelGGL(k_norm_f16q, dim3(rows), dim3(NORMQ_THREADS), (size_t)k * 4, s, x, (_Float16 *)x16, k, w, b,
-                     g_norm_stats);
+                     dev_stats());
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -201,9 +210,9 @@ int tables_get(DevTables *t) {
     g_dev_tab[dev].exp_f16 = p;
     g_dev_tab[dev].gelu_f16 = p + 65536;
     g_dev_tab_ok[dev] = true;
-    if (!g_norm_stats) {
-      VSIM_HIP(hipMalloc(&g_norm_stats, 4 * sizeof(unsigned)));
-      VSIM_HIP(hipMemset(g_norm_stats, 0, 4 * sizeof(unsigned)));
+    if (!g_dev_stats[dev]) {
+      VSIM_HIP(hipMalloc(&g_dev_stats[dev], 4 * sizeof(unsigned)));
+      VSIM_HIP(hipMemset(g_dev_stats[dev], 0, 4 * sizeof(unsigned)));
     }
   }
   *t = g_dev_tab[dev];
@@ -218,22 +227,39 @@ int tables_host(uint16_t *exp_f16, uint16_t *gelu_f16) {
   return VSIM_OK;
 }
 
-// g_norm_stats[2]: bounded cross-workgroup waits that gave up (k_layer_tail); 0 in a healthy run
-unsigned *spin_error_counter() { return g_norm_stats ? g_norm_stats + 2 : nullptr; }
-int spin_timeouts(unsigned *out) {
+unsigned *spin_error_counter() {
+  unsigned *st = dev_stats();
+  return st ? st + 2 : nullptr;
+}
+
+// counter k summed over every device that has one (hipMemcpy of a device word: a full sync of
+// that device's null stream, so call after the work to be checked has been synchronized)
+static int stats_sum(int k, unsigned *out) {
   *out = 0;
-  if (!g_norm_stats) return VSIM_OK;
-  VSIM_HIP(hipMemcpy(out, g_norm_stats + 2, sizeof(unsigned), hipMemcpyDeviceToHost));
+  int cur = 0;
+  VSIM_HIP(hipGetDevice(&cur));
+  for (int dev = 0; dev < 64; ++dev) {
+    if (!g_dev_stats[dev]) continue;
+    unsigned v = 0;
+    VSIM_HIP(hipSetDevice(dev));
+    VSIM_HIP(hipMemcpy(&v, g_dev_stats[dev] + k, sizeof(unsigned), hipMemcpyDeviceToHost));
+    *out += v;
+  }
+  VSIM_HIP(hipSetDevice(cur));
+  return VSIM_OK;
+}
+int spin_timeouts(unsigned *out) { return stats_sum(2, out); }
+int spin_timeouts_dev(int dev, unsigned *out) {
+  *out = 0;
+  if (dev < 0 || dev >= 64 || !g_dev_stats[dev]) return VSIM_OK;
+  VSIM_HIP(hipMemcpy(out, g_dev_stats[dev] + 2, sizeof(unsigned), hipMemcpyDeviceToHost));
   return VSIM_OK;
 }
 
 int norm_stats(unsigned *out2) {
-  if (!g_norm_stats) { out2[0] = out2[1] = 0; return VSIM_OK; }
-  unsigned h[4];
-  VSIM_HIP(hipMemcpy(h, g_norm_stats, sizeof(h), hipMemcpyDeviceToHost));
-  out2[0] = h[0];
-  out2[1] = h[1];
-  return VSIM_OK;
+  const int rc = stats_sum(0, &out2[0]);
+  if (rc != VSIM_OK) return rc;
+  return stats_sum(1, &out2[1]);
 }
 
 // ------------------------------------------------------------------ greedy argmax
