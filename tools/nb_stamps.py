@@ -1,0 +1,50 @@
+"""Where the barrier-free chain GEMVs wait (r05 diagnostic): GPT-J-6B exact decode on the
+VSIM_NB_STAMPS build (tools/build_variant.sh nbstamps Makefile 's/-fno-slp-vectorize$/& -DVSIM_NB_STAMPS/'),
+VSIM_TAIL_NB=3 VSIM_SOLO_NB=1, then the per-workgroup s_memtime sums of the last launches:
+the last layer's tail (fc_out tiles 0..127, out-projection tiles after the 16 heads) and the
+last per-layer k_gemv_solo_nb batch.  Prints medians per chunk (cycles of the shader clock)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from vsim_amd import hip  # noqa: E402
+from vsim_amd import modelgen as mg  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+arch_s, hp = mg.CONFIGS["gpt-j-6B"]
+m = hip.Model.create(hip.ARCH_GPTJ, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head, n_layer=hp.n_layer,
+                                         n_rot=hp.n_rot, use_parallel_residual=hp.use_parallel_residual),
+                     n_ctx=512, device=0)
+m.randomize(seed=1234, std=0.02)
+m.set_mode(hip.MODE_EXACT)
+m.set_graph(True)
+tok = int(np.argmax(m.eval(0, [50278, 12092, 2, 0, 50281])))
+m.generate(5, tok, steps)
+buf = np.zeros((2048, 32), np.uint64)
+f = hip.lib().vsim_debug_nb_stamps
+f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+assert f(buf.ctypes.data, buf.nbytes) == 0
+m.close()
+
+
+def role(name, rows, nprod, off):
+    b = buf[rows]
+    nch = np.maximum(b[:, 3].astype(float), 1)
+    dur = (b[:, 1] - b[:, 0]).astype(float)
+    print(f"{name}: {len(rows)} workgroups, chunks {int(np.median(nch))}, position {5 + steps}")
+    print(f"  consumer: {np.median(dur / nch):8.0f} cycles per chunk (p10 {np.percentile(dur / nch, 10):.0f}, "
+          f"p90 {np.percentile(dur / nch, 90):.0f}), waiting for producers {np.median(b[:, 2] / nch):6.0f}")
+    for k, what in enumerate(off):
+        v = b[:, what[1]:what[1] + nprod].astype(float) / nch[:, None]
+        print(f"  producers {what[0]:<10}: median {np.median(v):7.0f}  p90 {np.percentile(v, 90):7.0f} cycles per chunk")
+
+
+role("tail fc_out tiles", np.arange(0, 128), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
+role("tail out-proj tiles", np.arange(144, 272), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
+nsolo = 448 if os.environ.get("VSIM_SOLO_NB", "1") == "1" else 224
+role("k_gemv_solo_nb batch (fc_in, Q, K, V), first 64-row half", np.arange(1024, 1024 + nsolo), 6,
+     [("lgkm wait", 4), ("slot wait", 10), ("compute", 16)])

@@ -84,6 +84,7 @@ constexpr int C2_RING = 3, C2_WIN = 16;
 // ahead 34.8-34.9 (profiles/r04_tail_consumer_ab.txt)
 using C2Gemv = C2Shape<8, 4, false>;
 using C2Tail = C2Shape<16, 4, true>;
+using C2TailNB = C2Shape<16, 4, false>;  // (r05 A/B: producers on the consumer's SIMD too)
 
 template <class S>
 struct C2Lds {
@@ -277,26 +278,60 @@ __global__ void __launch_bounds__(C2Gemv::THREADS, 2) k_gemv_chain32(GemvBatch B
 // 32 adds they feed; the next chunk's ready count is read with the last batch.  Why: the
 // barrier version's per-chunk s_barrier and lgkmcnt(0) drain cost the chain 8.5 cycles per add
 // against the 4.3 the batched loop reaches alone (profiles/r04_cons_lat3.txt).
-// The 32 chain adds of one consumer batch (8 float4 in registers) as ONE volatile asm statement
-// with a memory clobber: the compiler keeps each batch's LDS reads in front of the adds they
-// overlap (left to itself it issued all of a chunk's reads first and spilled them), waits only for
-// the batch being added, and puts no s_nop between statements (it does between separate ones).
+// The chain adds of one consumer batch as volatile asm statements of 32 adds (8 float4 in
+// registers) with a memory clobber: the compiler keeps each batch's LDS reads in front of the adds
+// they overlap (left to itself it issued all of a chunk's reads first and spilled them), waits only
+// for the batch being added, and puts no s_nop inside a statement (it does between statements).
 #define NB_A4(i) "v_add_f32 %0, %0, %" #i "\n\t"
-#define NB_BATCH_ADDS(acc, cur)                                                                                 \
+#define NB_ADDS8(acc, a, o)                                                                                      \
   asm volatile(NB_A4(1) NB_A4(2) NB_A4(3) NB_A4(4) NB_A4(5) NB_A4(6) NB_A4(7) NB_A4(8) NB_A4(9) NB_A4(10) NB_A4(11) \
                    NB_A4(12) NB_A4(13) NB_A4(14) NB_A4(15) NB_A4(16) NB_A4(17) NB_A4(18) NB_A4(19) NB_A4(20)      \
                        NB_A4(21) NB_A4(22) NB_A4(23) NB_A4(24) NB_A4(25) NB_A4(26) NB_A4(27) NB_A4(28) NB_A4(29)  \
                            NB_A4(30) NB_A4(31) NB_A4(32)                                                         \
                : "+v"(acc)                                                                                       \
-               : "v"(cur[0].x), "v"(cur[0].y), "v"(cur[0].z), "v"(cur[0].w), "v"(cur[1].x), "v"(cur[1].y),       \
-                 "v"(cur[1].z), "v"(cur[1].w), "v"(cur[2].x), "v"(cur[2].y), "v"(cur[2].z), "v"(cur[2].w),       \
-                 "v"(cur[3].x), "v"(cur[3].y), "v"(cur[3].z), "v"(cur[3].w), "v"(cur[4].x), "v"(cur[4].y),       \
-                 "v"(cur[4].z), "v"(cur[4].w), "v"(cur[5].x), "v"(cur[5].y), "v"(cur[5].z), "v"(cur[5].w),       \
-                 "v"(cur[6].x), "v"(cur[6].y), "v"(cur[6].z), "v"(cur[6].w), "v"(cur[7].x), "v"(cur[7].y),       \
-                 "v"(cur[7].z), "v"(cur[7].w)                                                                    \
-               : "memory");                                                                                      \
-  _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) cur[j_] = nxt[j_]
+               : "v"(a[o].x), "v"(a[o].y), "v"(a[o].z), "v"(a[o].w), "v"(a[o + 1].x), "v"(a[o + 1].y),           \
+                 "v"(a[o + 1].z), "v"(a[o + 1].w), "v"(a[o + 2].x), "v"(a[o + 2].y), "v"(a[o + 2].z),            \
+                 "v"(a[o + 2].w), "v"(a[o + 3].x), "v"(a[o + 3].y), "v"(a[o + 3].z), "v"(a[o + 3].w),            \
+                 "v"(a[o + 4].x), "v"(a[o + 4].y), "v"(a[o + 4].z), "v"(a[o + 4].w), "v"(a[o + 5].x),            \
+                 "v"(a[o + 5].y), "v"(a[o + 5].z), "v"(a[o + 5].w), "v"(a[o + 6].x), "v"(a[o + 6].y),            \
+                 "v"(a[o + 6].z), "v"(a[o + 6].w), "v"(a[o + 7].x), "v"(a[o + 7].y), "v"(a[o + 7].z),            \
+                 "v"(a[o + 7].w)                                                                                 \
+               : "memory")
+#define NB_ADDS4(acc, a, o)                                                                                      \
+  asm volatile(NB_A4(1) NB_A4(2) NB_A4(3) NB_A4(4) NB_A4(5) NB_A4(6) NB_A4(7) NB_A4(8) NB_A4(9) NB_A4(10) NB_A4(11) \
+                   NB_A4(12) NB_A4(13) NB_A4(14) NB_A4(15) NB_A4(16)                                             \
+               : "+v"(acc)                                                                                       \
+               : "v"(a[o].x), "v"(a[o].y), "v"(a[o].z), "v"(a[o].w), "v"(a[o + 1].x), "v"(a[o + 1].y),           \
+                 "v"(a[o + 1].z), "v"(a[o + 1].w), "v"(a[o + 2].x), "v"(a[o + 2].y), "v"(a[o + 2].z),            \
+                 "v"(a[o + 2].w), "v"(a[o + 3].x), "v"(a[o + 3].y), "v"(a[o + 3].z), "v"(a[o + 3].w)             \
+               : "memory")
+// acc += the BQ float4 of cur in order (BQ a multiple of 4), then cur = nxt
+template <int BQ>
+__device__ __forceinline__ void nb_add_batch(float &acc, f32x4 (&cur)[BQ], const f32x4 (&nxt)[BQ]) {
+  static_assert(BQ % 4 == 0, "batches of 4 float4");
+#pragma unroll
+  for (int o = 0; o + 8 <= BQ; o += 8) NB_ADDS8(acc, cur, o);
+  if constexpr (BQ % 8 == 4) NB_ADDS4(acc, cur, BQ - 4);
+#pragma unroll
+  for (int j = 0; j < BQ; ++j) cur[j] = nxt[j];
+}
+// VSIM_NB_STAMPS (a diagnostic build, tools/build_variant.sh): per-workgroup s_memtime sums of
+// where the barrier-free GEMVs' waves wait, read back by vsim_debug_nb_stamps
+#ifdef VSIM_NB_STAMPS
+__device__ unsigned long long g_nb_stamps[2048][32];
+#define NBS(...) __VA_ARGS__
+#else
+#define NBS(...)
+#endif
 constexpr int NB_RING = 3;
+// float4 per consumer batch (the reads of the next batch are in flight during this one's adds;
+// lgkmcnt counts at most 15, so a batch stays below that with the counter read and the store)
+#ifndef NB_TAIL_BQ
+#define NB_TAIL_BQ 8
+#endif
+#ifndef NB_SOLO_BQ
+#define NB_SOLO_BQ 12
+#endif
 constexpr unsigned NB_SPIN_MAX = 1u << 24;
 template <class S>
 struct NbLds {
@@ -337,6 +372,7 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   if (wave > 0) {
     // ------------------------------------------------------------- producer
     const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
+    if (p >= NPW) return;  // (a launch wider than this shape needs)
     const int o = 2 * p + hb;  // this lane's block within the chunk
     const uint8_t *qs = B.j[ji].w.qs + (size_t)t * nb * T32 * 16 + (size_t)r * 16;
     const float *dd = B.j[ji].w.d + (size_t)t * nb * T32 + r;
@@ -352,25 +388,27 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
       else
         glds4<false>(xr + (size_t)b * QK, lds_addr(&L.RX[slot][p][0]));
     };
-    auto ldraw = [&](int c, uint4 &q, float &dq, f32x2 *xv) {
+    NBS(unsigned long long sw_dma = 0, sw_slot = 0, sw_comp = 0;)
+    // chunk c's raw block and factors from its DMA slot into registers (issued, not waited for:
+    // the reads complete behind the next chunk's pair terms)
+    // (factors: F0 / F1 = slots 0-15 / 16-31 of the half's block in every 16-lane row, for the
+    // DPP broadcast of pair_terms4_dpp: two 4-byte reads instead of eight 16-byte broadcasts)
+    const int fx = (lane & 32) + (lane & 15);
+    auto issue_raw = [&](int c, uint4 &q, float &dq, float &f0, float &f1) {
       const int slot = c % DEPTH;
-      __builtin_amdgcn_s_waitcnt(WAIT_VM);
+      NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
+      __builtin_amdgcn_s_waitcnt(WAIT_VM);  // this wave's DMA of chunk c landed
+      NBS(sw_dma += __builtin_amdgcn_s_memtime() - t0;)
       q = L.RQ[slot][p][lane];
       dq = L.RD[slot][p][lane];
-      const float4 *xq = (const float4 *)&L.RX[slot][p][hb * 32];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4 v = xq[i];
-        xv[2 * i].x = v.x;
-        xv[2 * i].y = v.y;
-        xv[2 * i + 1].x = v.z;
-        xv[2 * i + 1].y = v.w;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the slot is reloaded
-      dma(c + DEPTH);
+      f0 = L.RX[slot][p][fx];
+      f1 = L.RX[slot][p][fx + 16];
     };
-    auto compute = [&](int k, const f32x2 *xc, const uint4 &qc, float dqc) {
+    // chunk k's pair terms into ring slot k % NB_RING, then (lgkmcnt(0): the terms and the raw
+    // reads of chunk k+1 landed) the count, and the DMA of chunk k+1+DEPTH into the raw slot just read
+    auto compute = [&](int k, float f0, float f1, const uint4 &qc, float dqc) {
       const int slot = k % NB_RING;
+      NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
       if (k >= NB_RING) {
         unsigned spins = 0;
         while ((int)lds_load(&L.cons) < k - NB_RING + 1) {
@@ -382,43 +420,60 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
         }
         asm volatile("" ::: "memory");
       }
+      NBS(const unsigned long long t1 = __builtin_amdgcn_s_memtime(); sw_slot += t1 - t0;)
       const float dv = k * CB + o < nb ? dqc : 0.0f;
       const f32x2 d2 = {512.0f * dv, 512.0f * dv}, m2 = {-8.0f * dv, -8.0f * dv};
       float *dst = &L.P[slot][r * LD + o * 16];
-      const uint32_t qw[4] = {qc.x, qc.y, qc.z, qc.w};
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) {
-        float p4[4];
-        pair_terms4_x(qw[wv], d2, m2, xc + 4 * wv, p4);
-        *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the terms are in LDS before the count
+      float p4[4];
+      pair_terms4_dpp<0>(qc.x, d2, m2, f0, f1, p4);
+      *(float4 *)(dst + 0) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+      pair_terms4_dpp<1>(qc.y, d2, m2, f0, f1, p4);
+      *(float4 *)(dst + 4) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+      pair_terms4_dpp<2>(qc.z, d2, m2, f0, f1, p4);
+      *(float4 *)(dst + 8) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+      pair_terms4_dpp<3>(qc.w, d2, m2, f0, f1, p4);
+      *(float4 *)(dst + 12) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      NBS(sw_comp += __builtin_amdgcn_s_memtime() - t1;)
       if (lane == 0) __hip_atomic_fetch_add(&L.ready[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      dma(k + 1 + DEPTH);
     };
 #pragma unroll
     for (int c = 0; c < DEPTH; ++c) dma(c);
-    f32x2 xa[16], xb[16];
     uint4 qa, qb;
-    float da, db;
-    ldraw(0, qa, da, xa);
+    float da, db, fa0, fa1, fb0, fb1;
+    issue_raw(0, qa, da, fa0, fa1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    dma(DEPTH);
     for (int k = 0; k < nch; k += 2) {
-      ldraw(k + 1, qb, db, xb);
-      compute(k, xa, qa, da);
-      ldraw(k + 2, qa, da, xa);
-      if (k + 1 < nch) compute(k + 1, xb, qb, db);
+      issue_raw(k + 1, qb, db, fb0, fb1);
+      compute(k, fa0, fa1, qa, da);
+      issue_raw(k + 2, qa, da, fa0, fa1);
+      if (k + 1 < nch) compute(k + 1, fb0, fb1, qb, db);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
+    NBS(if (lane == 0 && p < 8) {
+      g_nb_stamps[blockIdx.x][4 + p] = sw_dma;
+      g_nb_stamps[blockIdx.x][12 + p] = sw_slot;
+      g_nb_stamps[blockIdx.x][20 + p] = sw_comp;
+      if (p < 4) g_nb_stamps[blockIdx.x][28 + p] = __builtin_amdgcn_s_memtime();
+    })
     return;
   }
 
   // --------------------------------------------------------------- consumer (lanes 0-31)
+  // Batches of 8 float4 (32 adds) in four register sets: the reads of batch q+3 go out with the
+  // adds of batch q, so a read has three batches (~100 adds) to land.  Batch q of a chunk always
+  // sits in set q % 4 (8 batches per chunk), so the sets need no copies across chunks.
   float acc = 0.0f;
   const int lr = lane & 31;
   constexpr int NV = S::CP / 4, BQ = 8, NBQ = NV / BQ;  // float4 per chunk, per batch, batches
-  static_assert(NV % BQ == 0 && NBQ >= 2, "batches tile the chunk");
+  static_assert(NV % BQ == 0 && NBQ % 4 == 0, "batches tile the chunk in whole rounds of four sets");
   auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
+  NBS(unsigned long long cw = 0;)
   auto wait_ready = [&](int c, unsigned have) {
     unsigned spins = 0;
+    NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
     while (have < need(c)) {
       have = lds_load(&L.ready[c % NB_RING]);
       if (++spins == NB_SPIN_MAX) {
@@ -426,37 +481,46 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
         break;
       }
     }
+    NBS(cw += __builtin_amdgcn_s_memtime() - t0;)
     asm volatile("" ::: "memory");
   };
   __builtin_amdgcn_s_setprio(3);
+  NBS(const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();)
   wait_ready(0, 0u);
-  f32x4 cur[BQ], nxt[BQ];
-  {
-    const f32x4 *p0 = (const f32x4 *)&L.P[0][lr * LD];
+  f32x4 b0[BQ], b1[BQ], b2[BQ], b3[BQ];
+  auto rd = [&](f32x4 (&d)[BQ], int c, int q) {  // batch q of chunk c (past the last chunk: harmless)
+    const f32x4 *src = (const f32x4 *)&L.P[c % NB_RING][lr * LD] + q * BQ;
 #pragma unroll
-    for (int j = 0; j < BQ; ++j) cur[j] = p0[j];
-  }
-  static_assert(BQ == 8, "NB_BATCH_ADDS adds 8 float4");
-  auto adds = [&]() { NB_BATCH_ADDS(acc, cur); };
+    for (int j = 0; j < BQ; ++j) d[j] = src[j];
+  };
+  rd(b0, 0, 0);
+  rd(b1, 0, 1);
+  rd(b2, 0, 2);
   for (int c = 0; c < nch; ++c) {
-    const f32x4 *pc = (const f32x4 *)&L.P[c % NB_RING][lr * LD];
-    unsigned rdy = 0;
+    // the next chunk's count, read first: compared at batch NBQ-3 (before that chunk's first read),
+    // by when every read issued after it has had batches to land (a poll at the chunk's end
+    // drained the whole read pipeline: lgkmcnt(0) at its loop head)
+    const unsigned rdy = lds_load(&L.ready[(c + 1) % NB_RING]);
 #pragma unroll
-    for (int q = 0; q < NBQ - 1; ++q) {
-#pragma unroll
-      for (int j = 0; j < BQ; ++j) nxt[j] = pc[(q + 1) * BQ + j];
-      if (q == NBQ - 2) rdy = lds_load(&L.ready[(c + 1) % NB_RING]);  // (past the last chunk: unused)
-      adds();
+    for (int q = 0; q < NBQ; ++q) {
+      const int qn = q + 3, cn = qn < NBQ ? c : c + 1, qr = qn < NBQ ? qn : qn - NBQ;
+      if (qn == NBQ && c + 1 < nch && rdy < need(c + 1)) wait_ready(c + 1, rdy);
+      asm volatile("" ::: "memory");
+      f32x4(&dst)[BQ] = (qn % 4 == 0) ? b0 : (qn % 4 == 1) ? b1 : (qn % 4 == 2) ? b2 : b3;
+      rd(dst, cn, qr);
+      f32x4(&cur)[BQ] = (q % 4 == 0) ? b0 : (q % 4 == 1) ? b1 : (q % 4 == 2) ? b2 : b3;
+      NB_ADDS8(acc, cur, 0);
+      if (q == NBQ - 1)  // the chunk's last reads landed (the adds waited for them): refill its slot
+        __hip_atomic_store(&L.cons, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // the chunk's last batch is in registers: its slot may be refilled
-    __hip_atomic_store(&L.cons, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (c + 1 < nch) wait_ready(c + 1, rdy);
-    const f32x4 *pn = (const f32x4 *)&L.P[(c + 1) % NB_RING][lr * LD];  // (past the last chunk: harmless)
-#pragma unroll
-    for (int j = 0; j < BQ; ++j) nxt[j] = pn[j];
-    adds();
   }
   __builtin_amdgcn_s_setprio(0);
+  NBS(if (lane == 0) {
+    g_nb_stamps[blockIdx.x][0] = c_t0;
+    g_nb_stamps[blockIdx.x][1] = __builtin_amdgcn_s_memtime();
+    g_nb_stamps[blockIdx.x][2] = cw;
+    g_nb_stamps[blockIdx.x][3] = nch;
+  })
 
   // ----------------------------------------------------------------- epilogue
   const int row = t * T32 + lr;
@@ -516,7 +580,9 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   } L;
   int b = blockIdx.x;
   if (b < T.nf) {
-    if constexpr (NBM & 1)
+    if constexpr ((NBM & 5) == 5)
+      chain32_nb_body<C2TailNB, false>(T.f, b, *(NbLds<C2TailNB> *)&L.n, T.err);
+    else if constexpr (NBM & 1)
       chain32_nb_body<C2Tail, false>(T.f, b, L.n, T.err);
     else
       chain32_body(T.f, b, L.g);
@@ -572,13 +638,14 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   // no CU start as attention heads end
   static const int nbm = [] {
     const char *e = getenv("VSIM_TAIL_NB");
-    return e ? atoi(e) & 3 : 0;
+    return e ? atoi(e) & 7 : 0;
   }();
   const dim3 grid(T.nf + a.H * S + no), blk(C2Tail::THREADS);
   if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, 8192, s, T);
   if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, 8192, s, T);
   if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, 8192, s, T);
   if (nbm == 3) hipLaunchKernelGGL(k_layer_tail<3>, grid, blk, 8192, s, T);
+  if (nbm == 7) hipLaunchKernelGGL(k_layer_tail<7>, grid, blk, 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -776,16 +843,18 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
 // waits for the consumer's count before overwriting a slot; the consumer reads in batches of 8.
 // r02's barrier-free variant (per-slot counters too) lost to the barrier with the one-read-per-4-
 // adds consumer; r05 measures it again with the batched consumer.
-template <int CB, int PF>
-__device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*P)[64 * SoloShape<CB, 1>::LD],
-                                             unsigned *ready, unsigned *consw, unsigned *err) {
-  using S = SoloShape<CB, 1>;
-  constexpr int LD = S::LD;
+// CONS = 2: 128 rows, the two consumers (waves 0 and 4) on one SIMD, twelve producers on the other
+// three; each 64-row half has its own ready counters and consumer count.
+template <int CB, int PF, int CONS>
+__device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*P)[SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD],
+                                             unsigned (*ready)[NB_RING], unsigned *consw, unsigned *err) {
+  using S = SoloShape<CB, CONS>;
+  constexpr int LD = S::LD, TPG = 2 * CONS;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   int ji = 0;
   while (ji < B.nj) {
-    const int ng = (B.j[ji].w.tiles + 1) / 2;
+    const int ng = (B.j[ji].w.tiles + TPG - 1) / TPG;
     if (g < ng) break;
     g -= ng;
     ++ji;
@@ -794,16 +863,17 @@ __device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*
   ji = __builtin_amdgcn_readfirstlane(ji);
   g = __builtin_amdgcn_readfirstlane(g);
   const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
-  if (threadIdx.x < NB_RING) ready[threadIdx.x] = 0;
-  if (threadIdx.x == 0) *consw = 0;
+  if (threadIdx.x < CONS * NB_RING) (&ready[0][0])[threadIdx.x] = 0;
+  if (threadIdx.x < CONS) consw[threadIdx.x] = 0;
   __syncthreads();
-  if ((wave & 3) == 0 && wave > 0) return;  // the consumer's SIMD is left to it
+  if ((wave & 3) == 0 && (wave >> 2) >= CONS) return;  // the consumers' SIMD is left to them
 
-  if (wave != 0) {
+  if ((wave & 3) != 0) {
     // ------------------------------------------------------------- producer
-    const int o = wave - 1 - (wave >> 2);  // block of the chunk: waves 1,2,3,5,6,7 -> 0..5
+    const int pi = wave - 1 - (wave >> 2);  // waves 1,2,3,5,6,7,9,... -> 0,1,2,...
+    const int o = pi % CB, c = pi / CB;     // block of the chunk, the 64-row half (consumer) served
     const int h = lane >> 5, r = lane & 31;
-    const int tile = 2 * g + h;
+    const int tile = TPG * g + 2 * c + h;
     const bool tile_ok = tile < tiles;
     const int tl = tile_ok ? tile : tiles - 1;
     const uint8_t *qs = B.j[ji].w.qs + ((size_t)tl * nb * T32 + r) * 16;
@@ -823,19 +893,22 @@ __device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*
         xv[i].y = xp[2 * i + 1];
       }
     };
-    auto signal = [&](int c) {  // chunk c's terms are in LDS (after an lgkmcnt(0))
-      if (lane == 0) __hip_atomic_fetch_add(&ready[c % NB_RING], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    auto signal = [&](int k) {  // chunk k's terms are in LDS (after an lgkmcnt(0))
+      if (lane == 0) __hip_atomic_fetch_add(&ready[c][k % NB_RING], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
+    NBS(unsigned long long sw_f = 0, sw_slot = 0, sw_comp = 0;)
     auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
       ld(k + PF, qn, dqn);
+      NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this chunk's factors, the last chunk's stores
       __builtin_amdgcn_sched_barrier(0);
+      NBS(const unsigned long long t1 = __builtin_amdgcn_s_memtime(); sw_f += t1 - t0;)
       if (k > 0) signal(k - 1);
       ldx(k + 1, xn);
       __builtin_amdgcn_sched_barrier(0);
       if (k >= NB_RING) {  // slot k % NB_RING: the consumer is done with chunk k - NB_RING
         unsigned spins = 0;
-        while ((int)lds_load(consw) < k - NB_RING + 1) {
+        while ((int)lds_load(&consw[c]) < k - NB_RING + 1) {
           __builtin_amdgcn_s_sleep(1);
           if (++spins == NB_SPIN_MAX) {
             if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -844,13 +917,14 @@ __device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*
         }
         asm volatile("" ::: "memory");
       }
+      NBS(const unsigned long long t2 = __builtin_amdgcn_s_memtime(); sw_slot += t2 - t1;)
       const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
       const float dl = 512.0f * dv, ml = -8.0f * dv;
       float dh, mh;
       asm("v_mov_b32 %0, %1" : "=v"(dh) : "v"(dl));  // (as in solo_body)
       asm("v_mov_b32 %0, %1" : "=v"(mh) : "v"(ml));
       const f32x2 d2 = {dl, dh}, m2 = {ml, mh};
-      float *dst = &P[k % NB_RING][lane * LD + o * 16];
+      float *dst = &P[k % NB_RING][(64 * c + lane) * LD + o * 16];
 #pragma unroll
       for (int wv = 0; wv < 4; ++wv) {
         float p4[4];
@@ -858,6 +932,7 @@ __device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*
         *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      NBS(sw_comp += __builtin_amdgcn_s_memtime() - t2;)
     };
     u32x4 q[PF + 1];
     float e[PF + 1];
@@ -875,55 +950,71 @@ __device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     signal(nch - 1);
+    NBS(if (lane == 0 && B.nj > 1 && c == 0) {  // (rows 1024.. : the tail owns 0..)
+      g_nb_stamps[1024 + blockIdx.x][4 + o] = sw_f;
+      g_nb_stamps[1024 + blockIdx.x][10 + o] = sw_slot;
+      g_nb_stamps[1024 + blockIdx.x][16 + o] = sw_comp;
+      g_nb_stamps[1024 + blockIdx.x][22 + o] = __builtin_amdgcn_s_memtime();
+    })
     return;
   }
 
-  // --------------------------------------------------------------- consumer (64 rows)
+  // --------------------------------------------------------------- consumer (64 rows each)
   float acc = 0.0f;
-  constexpr int NV = S::CP / 4, BQ = 8, NBQ = NV / BQ, NPW = CB;
+  const int cw_i = wave >> 2, crow = 64 * cw_i + lane;  // this consumer's half, its row in the group
+  constexpr int NV = S::CP / 4, BQ = NB_SOLO_BQ, NBQ = NV / BQ, NPW = CB;
   static_assert(NV % BQ == 0 && NBQ >= 2, "batches tile the chunk");
   auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
+  NBS(unsigned long long cw = 0;)
   auto wait_ready = [&](int c, unsigned have) {
     unsigned spins = 0;
+    NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
     while (have < need(c)) {
-      have = lds_load(&ready[c % NB_RING]);
+      have = lds_load(&ready[cw_i][c % NB_RING]);
       if (++spins == NB_SPIN_MAX) {
         if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
+    NBS(cw += __builtin_amdgcn_s_memtime() - t0;)
     asm volatile("" ::: "memory");
   };
   __builtin_amdgcn_s_setprio(3);
+  NBS(const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();)
   wait_ready(0, 0u);
   f32x4 cur[BQ], nxt[BQ];
   {
-    const f32x4 *p0 = (const f32x4 *)&P[0][lane * LD];
+    const f32x4 *p0 = (const f32x4 *)&P[0][crow * LD];
 #pragma unroll
     for (int j = 0; j < BQ; ++j) cur[j] = p0[j];
   }
-  static_assert(BQ == 8, "NB_BATCH_ADDS adds 8 float4");
-  auto adds = [&]() { NB_BATCH_ADDS(acc, cur); };
+  auto adds = [&]() { nb_add_batch<BQ>(acc, cur, nxt); };
   for (int c = 0; c < nch; ++c) {
-    const f32x4 *pc = (const f32x4 *)&P[c % NB_RING][lane * LD];
-    unsigned rdy = 0;
+    const f32x4 *pc = (const f32x4 *)&P[c % NB_RING][crow * LD];
+    const unsigned rdy = lds_load(&ready[cw_i][(c + 1) % NB_RING]);  // (as in chain32_nb_body)
 #pragma unroll
     for (int q = 0; q < NBQ - 1; ++q) {
 #pragma unroll
       for (int j = 0; j < BQ; ++j) nxt[j] = pc[(q + 1) * BQ + j];
-      if (q == NBQ - 2) rdy = lds_load(&ready[(c + 1) % NB_RING]);
       adds();
     }
-    __hip_atomic_store(consw, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (c + 1 < nch) wait_ready(c + 1, rdy);
-    const f32x4 *pn = (const f32x4 *)&P[(c + 1) % NB_RING][lane * LD];
+    __hip_atomic_store(&consw[cw_i], (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (c + 1 < nch && rdy < need(c + 1)) wait_ready(c + 1, rdy);
+    asm volatile("" ::: "memory");
+    const f32x4 *pn = (const f32x4 *)&P[(c + 1) % NB_RING][crow * LD];
 #pragma unroll
     for (int j = 0; j < BQ; ++j) nxt[j] = pn[j];
     adds();
   }
+  NBS(if (lane == 0 && B.nj > 1 && cw_i == 0) {
+    g_nb_stamps[1024 + blockIdx.x][0] = c_t0;
+    g_nb_stamps[1024 + blockIdx.x][1] = __builtin_amdgcn_s_memtime();
+    g_nb_stamps[1024 + blockIdx.x][2] = cw;
+    g_nb_stamps[1024 + blockIdx.x][3] = nch;
+  })
 
   // ----------------------------------------------------------------- epilogue
-  const int row = g * S::ROWS + lane;
+  const int row = g * S::ROWS + crow;
   const int rows = B.j[ji].w.rows;
   const float *bias = B.j[ji].bias;
   float *y = B.j[ji].y;
@@ -943,11 +1034,11 @@ __device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int CB, int PF>
-__global__ void __launch_bounds__((64 * SoloShape<CB, 1>::WAVES), 1) k_gemv_solo_nb(GemvBatch B, unsigned *err) {
-  __shared__ __attribute__((aligned(16))) float P[NB_RING][64 * SoloShape<CB, 1>::LD];
-  __shared__ unsigned ready[NB_RING], consw;
-  solo_nb_body<CB, PF>(B, blockIdx.x, P, ready, &consw, err);
+template <int CB, int PF, int CONS>
+__global__ void __launch_bounds__((64 * SoloShape<CB, CONS>::WAVES), 1) k_gemv_solo_nb(GemvBatch B, unsigned *err) {
+  __shared__ __attribute__((aligned(16))) float P[NB_RING][SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD];
+  __shared__ unsigned ready[CONS][NB_RING], consw[CONS];
+  solo_nb_body<CB, PF, CONS>(B, blockIdx.x, P, ready, consw, err);
 }
 
 template <int CB, int PF, int CONS>
@@ -981,13 +1072,16 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     tiles += B.j[i].w.tiles;
   }
   if (tiles == 0) return VSIM_OK;
-  static const bool solo_nb = [] {
+  static const int solo_nb = [] {
     const char *e = getenv("VSIM_SOLO_NB");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) : 0;
   }();
-  if (gemv_chain_solo(B) && solo_nb) {
-    hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF>), dim3(solo_groups(B)),
+  if (gemv_chain_solo(B) && solo_nb == 1) {
+    hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)),
                        dim3(64 * SoloShape<SOLO_CB, 1>::WAVES), 0, s, B, spin_error_counter());
+  } else if (gemv_chain_solo(B) && solo_nb == 2) {
+    hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF, 2>), dim3(solo_groups(B, 2)),
+                       dim3(64 * SoloShape<SOLO_CB, 2>::WAVES), 0, s, B, spin_error_counter());
   } else if (gemv_chain_solo(B)) {
     hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)), dim3(64 * SoloShape<SOLO_CB, 1>::WAVES),
                        0, s, B);
@@ -999,3 +1093,10 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
 }
 
 }  // namespace vsim
+
+#ifdef VSIM_NB_STAMPS
+extern "C" int vsim_debug_nb_stamps(void *dst, size_t bytes) {
+  if (bytes > sizeof(vsim::g_nb_stamps)) bytes = sizeof(vsim::g_nb_stamps);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(vsim::g_nb_stamps), bytes) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -126,6 +126,31 @@ __device__ __forceinline__ void pair_terms4_x(uint32_t w, f32x2 d512, f32x2 m2, 
   p4[3] = t23.y;
 }
 
+// The same four terms with the activation factors broadcast by DPP instead of held per lane: a
+// half-wave works on one block, and its 32 factors sit in two VGPRs, F0 = memory slots 0-15 and
+// F1 = slots 16-31 of its block in each 16-lane row (rows 0-1: the lower half's block, rows 2-3:
+// the upper half's).  row_newbcast:n hands every lane of a row that row's lane n, folded into the
+// v_mul_f32 that uses it, so a product costs one plain multiply and no factor registers or LDS
+// broadcast reads; the products and sums round exactly as pair_terms4_x's packed ones.
+template <int POS>
+__device__ __forceinline__ float xbcast(float f0, float f1) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(POS < 16 ? f0 : f1), 0x150 + (POS & 15), 0xF, 0xF,
+                                                    false));
+}
+template <int W>  // word W of the block: pairs 4W .. 4W+3, natural factor elements 8W .. 8W+7
+__device__ __forceinline__ void pair_terms4_dpp(uint32_t w, f32x2 d512, f32x2 m2, float F0, float F1, float *p4) {
+  const int lo = (int)(w & 0x0F0F0F0Fu), hi = (int)((w >> 4) & 0x0F0F0F0Fu);
+  const f32x2 f01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, false), d512, m2);
+  const f32x2 g01 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, false), d512, m2);
+  const f32x2 f23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(lo, true), d512, m2);
+  const f32x2 g23 = __builtin_elementwise_fma(__builtin_amdgcn_cvt_pk_f32_fp8(hi, true), d512, m2);
+  // pair 4W + k takes natural elements 8W + 2k (first factor) and 8W + 2k + 1, at memory slots xd_slot()
+  p4[0] = xbcast<xd_slot(8 * W + 0)>(F0, F1) * f01.x + xbcast<xd_slot(8 * W + 1)>(F0, F1) * g01.x;
+  p4[1] = xbcast<xd_slot(8 * W + 2)>(F0, F1) * f01.y + xbcast<xd_slot(8 * W + 3)>(F0, F1) * g01.y;
+  p4[2] = xbcast<xd_slot(8 * W + 4)>(F0, F1) * f23.x + xbcast<xd_slot(8 * W + 5)>(F0, F1) * g23.x;
+  p4[3] = xbcast<xd_slot(8 * W + 6)>(F0, F1) * f23.y + xbcast<xd_slot(8 * W + 7)>(F0, F1) * g23.y;
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
 
 // LDS-DMA: each lane's 16 (4) bytes from its own global address land lane-linearly at the
