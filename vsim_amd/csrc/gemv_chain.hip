@@ -84,7 +84,6 @@ constexpr int C2_RING = 3, C2_WIN = 16;
 // ahead 34.8-34.9 (profiles/r04_tail_consumer_ab.txt)
 using C2Gemv = C2Shape<8, 4, false>;
 using C2Tail = C2Shape<16, 4, true>;
-using C2TailNB = C2Shape<16, 4, false>;  // (r05 A/B: producers on the consumer's SIMD too)
 
 template <class S>
 struct C2Lds {
@@ -580,9 +579,7 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   } L;
   int b = blockIdx.x;
   if (b < T.nf) {
-    if constexpr ((NBM & 5) == 5)
-      chain32_nb_body<C2TailNB, false>(T.f, b, *(NbLds<C2TailNB> *)&L.n, T.err);
-    else if constexpr (NBM & 1)
+    if constexpr (NBM & 1)
       chain32_nb_body<C2Tail, false>(T.f, b, L.n, T.err);
     else
       chain32_body(T.f, b, L.g);
@@ -636,16 +633,19 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   // one workgroup per CU (fc_out's consumer keeps its SIMD): the static LDS is above half the
   // CU's already at DEPTH 8, the dynamic pad keeps it so at any depth; the workgroups that find
   // no CU start as attention heads end
+  // the barrier-free hand-off (chain32_nb_body) for fc_out and the out-projection; r05 A/B
+  // against the per-chunk barrier (chain32_body): 31.4 vs 33.7 us per tail, 630-631 vs 605-607
+  // tok/s (profiles/r05_tail_nb_ab.txt).  VSIM_TAIL_NB = 0 (barrier), 1 (fc_out only), 2
+  // (out-projection only) rebuild the A/B.
   static const int nbm = [] {
     const char *e = getenv("VSIM_TAIL_NB");
-    return e ? atoi(e) & 7 : 0;
+    return e ? atoi(e) & 3 : 3;
   }();
   const dim3 grid(T.nf + a.H * S + no), blk(C2Tail::THREADS);
   if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, 8192, s, T);
   if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, 8192, s, T);
   if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, 8192, s, T);
   if (nbm == 3) hipLaunchKernelGGL(k_layer_tail<3>, grid, blk, 8192, s, T);
-  if (nbm == 7) hipLaunchKernelGGL(k_layer_tail<7>, grid, blk, 8192, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
