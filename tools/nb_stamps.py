@@ -44,7 +44,30 @@ def role(name, rows, nprod, off):
 
 
 role("tail fc_out tiles", np.arange(0, 128), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
-role("tail out-proj tiles", np.arange(144, 272), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
-nsolo = 448 if os.environ.get("VSIM_SOLO_NB", "1") == "1" else 224
-role("k_gemv_solo_nb batch (fc_in, Q, K, V), first 64-row half", np.arange(1024, 1024 + nsolo), 6,
-     [("lgkm wait", 4), ("slot wait", 10), ("compute", 16)])
+role("tail out-proj tiles", np.arange(144 + (128 if os.environ.get("VSIM_TAIL_QKV", "1") != "0" else 0), 272 + (128 if os.environ.get("VSIM_TAIL_QKV", "1") != "0" else 0)), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
+nsolo = 0  # (k_gemv_solo_nb is not in the r05 decode path)
+if nsolo:
+    role("k_gemv_solo_nb batch (fc_in, Q, K, V), first 64-row half", np.arange(1024, 1024 + nsolo), 6,
+         [("lgkm wait", 4), ("slot wait", 10), ("compute", 16)])
+
+# the last tail's timeline (s_memrealtime, 100 MHz; rows 1536 + workgroup): fc_out tiles, QKV
+# workgroups (three consumers' ends), heads (count reached, end), out-projection (count, end)
+nf, nq = 128, (128 if os.environ.get("VSIM_TAIL_QKV", "1") != "0" else 0)
+na, no = 16, 128
+tl = buf[1536:1536 + nf + nq + na + no, :4].astype(np.int64)
+t0 = tl[:, 0].min()
+us = lambda v: (v - t0) / 100.0  # noqa: E731
+
+
+def tlrow(name, rows, cols):
+    r = tl[rows]
+    print(f"{name:10s} start med {np.median(us(r[:, 0])):6.2f} max {us(r[:, 0]).max():6.2f} us" +
+          "".join(f" | {c} med {np.median(us(r[:, i])):6.2f} max {us(r[:, i]).max():6.2f}" for c, i in cols))
+
+
+print("tail timeline (us from the first workgroup's start):")
+tlrow("fc_out", np.arange(0, nf), [("end", 2)])
+if nq:
+    tlrow("QKV", np.arange(nf, nf + nq), [("Q end", 1), ("K end", 2), ("V end", 3)])
+tlrow("heads", np.arange(nf + nq, nf + nq + na), [("ready", 1), ("end", 2)])
+tlrow("out-proj", np.arange(nf + nq + na, nf + nq + na + no), [("ready", 1), ("end", 2)])

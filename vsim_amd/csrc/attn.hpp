@@ -25,7 +25,14 @@ constexpr int ATT_DPL = 4;      // max float4 of the head dimension per lane in 
 // and softmax (identical in each), then the KQV chains and quantization of output columns
 // [part*c, part*c + c), c = d / S, so a head's V rows spread over S CUs.  Every part writes
 // the same new K/V cache row (identical bytes) before reading it back.
-template <int NT, bool CO = false>
+// CI: q, k, v were stored write-through by other workgroups of this launch (k_layer_tail's
+// QKV role): read them device-coherent (sc1), past any stale line in this XCD's L2.
+template <bool CI>
+__device__ __forceinline__ float ld_in(const float *p) {
+  if constexpr (CI) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <int NT, bool CO = false, bool CI = false>
 __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   constexpr int ATT_THREADS = NT, ATT_WAVES = NT / 64;
   const int S = A.nsplit > 1 ? A.nsplit : 1, h = hs / S, part = hs % S;
@@ -39,9 +46,9 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   __shared__ double shd[ATT_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < d; i += ATT_THREADS) {
-    qh[i] = A.q[h * d + i];
-    kh[i] = A.k[h * d + i];
-    A.vc[(size_t)n_past * E + h * d + i] = A.v[h * d + i];
+    qh[i] = ld_in<CI>(A.q + h * d + i);
+    kh[i] = ld_in<CI>(A.k + h * d + i);
+    A.vc[(size_t)n_past * E + h * d + i] = ld_in<CI>(A.v + h * d + i);
   }
   __syncthreads();
   // RoPE (ggml.c:6117-6152 / 5952-5973), position p = n_past for both q (mode 0) and k
