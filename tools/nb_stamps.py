@@ -44,7 +44,7 @@ def role(name, rows, nprod, off):
 
 
 role("tail fc_out tiles", np.arange(0, 128), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
-role("tail out-proj tiles", np.arange(144 + (128 if os.environ.get("VSIM_TAIL_QKV", "1") != "0" else 0), 272 + (128 if os.environ.get("VSIM_TAIL_QKV", "1") != "0" else 0)), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
+role("tail out-proj tiles", np.arange(144 + (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0), 272 + (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0)), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
 nsolo = 0  # (k_gemv_solo_nb is not in the r05 decode path)
 if nsolo:
     role("k_gemv_solo_nb batch (fc_in, Q, K, V), first 64-row half", np.arange(1024, 1024 + nsolo), 6,
@@ -52,7 +52,7 @@ if nsolo:
 
 # the last tail's timeline (s_memrealtime, 100 MHz; rows 1536 + workgroup): fc_out tiles, QKV
 # workgroups (three consumers' ends), heads (count reached, end), out-projection (count, end)
-nf, nq = 128, (128 if os.environ.get("VSIM_TAIL_QKV", "1") != "0" else 0)
+nf, nq = 128, (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0)
 na, no = 16, 128
 tl = buf[1536:1536 + nf + nq + na + no, :4].astype(np.int64)
 t0 = tl[:, 0].min()
@@ -69,5 +69,11 @@ print("tail timeline (us from the first workgroup's start):")
 tlrow("fc_out", np.arange(0, nf), [("end", 2)])
 if nq:
     tlrow("QKV", np.arange(nf, nf + nq), [("Q end", 1), ("K end", 2), ("V end", 3)])
-tlrow("heads", np.arange(nf + nq, nf + nq + na), [("ready", 1), ("end", 2)])
+tlrow("heads", np.arange(nf + nq, nf + nq + na), [("attn", 1), ("end", 2)])
 tlrow("out-proj", np.arange(nf + nq + na, nf + nq + na + no), [("ready", 1), ("end", 2)])
+# the heads' phases (ATT_STAMP: columns 4-7 = KQ, softmax, KQV, quantize starts; 1 = done)
+hr = tl[nf + nq:nf + nq + na]
+ph = buf[1536 + nf + nq:1536 + nf + nq + na, 4:8].astype(np.int64)
+print("heads phases (us, medians): setup+RoPE %.2f  KQ %.2f  softmax %.2f  KQV %.2f  quantize %.2f" % (
+    np.median(ph[:, 0] - hr[:, 0]) / 100, np.median(ph[:, 1] - ph[:, 0]) / 100, np.median(ph[:, 2] - ph[:, 1]) / 100,
+    np.median(ph[:, 3] - ph[:, 2]) / 100, np.median(hr[:, 1] - ph[:, 3]) / 100))

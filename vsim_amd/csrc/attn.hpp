@@ -10,6 +10,11 @@
 
 namespace vsim {
 
+// (diagnostic builds define ATT_STAMP(i) to stamp the phases of a head; nothing otherwise)
+#ifndef ATT_STAMP
+#define ATT_STAMP(i)
+#endif
+
 // One workgroup per head.  KQ: 16 lanes per key (four keys per wave instruction, KB
 // steps loaded at once), products over the head dimension summed as a tree in double; the
 // reference's sequential double sum lies within 2*d*2^-53*sum|p| of it, so when both ends of
@@ -25,14 +30,7 @@ constexpr int ATT_DPL = 4;      // max float4 of the head dimension per lane in 
 // and softmax (identical in each), then the KQV chains and quantization of output columns
 // [part*c, part*c + c), c = d / S, so a head's V rows spread over S CUs.  Every part writes
 // the same new K/V cache row (identical bytes) before reading it back.
-// CI: q, k, v were stored write-through by other workgroups of this launch (k_layer_tail's
-// QKV role): read them device-coherent (sc1), past any stale line in this XCD's L2.
-template <bool CI>
-__device__ __forceinline__ float ld_in(const float *p) {
-  if constexpr (CI) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return *p;
-}
-template <int NT, bool CO = false, bool CI = false>
+template <int NT, bool CO = false>
 __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   constexpr int ATT_THREADS = NT, ATT_WAVES = NT / 64;
   const int S = A.nsplit > 1 ? A.nsplit : 1, h = hs / S, part = hs % S;
@@ -46,9 +44,9 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   __shared__ double shd[ATT_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < d; i += ATT_THREADS) {
-    qh[i] = ld_in<CI>(A.q + h * d + i);
-    kh[i] = ld_in<CI>(A.k + h * d + i);
-    A.vc[(size_t)n_past * E + h * d + i] = ld_in<CI>(A.v + h * d + i);
+    qh[i] = A.q[h * d + i];
+    kh[i] = A.k[h * d + i];
+    A.vc[(size_t)n_past * E + h * d + i] = A.v[h * d + i];
   }
   __syncthreads();
   // RoPE (ggml.c:6117-6152 / 5952-5973), position p = n_past for both q (mode 0) and k
@@ -75,6 +73,7 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   // waves), not only by the threads that stored it: the barrier (its release drains the stores)
   // orders them.  r05: until then that read raced the store whenever n_past >= 16.
   __syncthreads();
+  ATT_STAMP(0);
   // KQ[k] = (float) sum_i (double)(K[k][i] * q[i]) in order i = 0..d-1; then * scale.
   // Row r (lanes 16r..16r+15) of a wave takes one key per step; lane l16 covers the float4s
   // at 4*l16 + 64*e of the head dimension.  A wave loads ATT_KB steps (4*ATT_KB keys) at once.
@@ -139,6 +138,7 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
       }
     }
   }
+  ATT_STAMP(1);
   // max, exp via table, exact double sum (fp16 values: any order), 1/sum
   mx = wave_max_f(mx);
   if (lane == 0) shf[wid] = mx;
@@ -159,6 +159,7 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
   const float inv = (float)(1.0 / sum);
   for (int k = tid; k < nk; k += ATT_THREADS) pr[k] = pr[k] * inv;
   __syncthreads();
+  ATT_STAMP(2);
   // KQV: y[dd] = sum_k V[k][dd] * p[k], sequential float chain from 0.0f (product and sum
   // rounded separately), thread j < c for column dd = c0 + j.  Every thread loads V tiles
   // (KT keys x c floats, float4 per slot) three tiles ahead into registers and stores them
@@ -234,6 +235,7 @@ __device__ __forceinline__ void attn_body(const AttnJob &A, int hs, float *sm) {
     }
     if (tid < c && A.out) st_out<CO>(A.out + h * d + c0 + tid, y);
   }
+  ATT_STAMP(3);
   // quantize the part's outputs: wave w holds columns c0 + 64w .. +63, two 32-blocks
   if (wid * 64 < c) {
     const int blk = (h * d + c0 + wid * 64) / QK + (lane >> 5);

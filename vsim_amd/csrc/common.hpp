@@ -341,11 +341,8 @@ int attn_prefill_ldt(int nk);  // V^T row length (keys padded to the key tile)
 _Float16 *attn_prefill_k16(void *scratch, int E, int nk);
 _Float16 *attn_prefill_vt16(void *scratch, int E, int nk);
 size_t attn_prefill_scratch(int E, int nk);
-// fused layer tail (gemv_chain.hip): fc_out f beside {Q, K, V} q (optional: q.nj = 0 when they ran
-// before), the attention heads and the out-projection o; done[0] / done[64]: launch counters
-// (zeroed by the layer's k_ln_quant)
-int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const GemvBatch &q, const AttnJob &a, unsigned *done,
-                      int n_ctx, hipStream_t s);
+int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
+                      hipStream_t s);
 int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
 int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s,

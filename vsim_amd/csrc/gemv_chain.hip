@@ -21,6 +21,16 @@
 #include <cstdlib>
 #include <cstring>
 
+// VSIM_NB_STAMPS (a diagnostic build, tools/build_variant.sh): per-workgroup s_memtime sums of
+// where the barrier-free GEMVs' waves wait, an s_memrealtime timeline of the layer tail's roles
+// and the attention heads' phases, read back by vsim_debug_nb_stamps (tools/nb_stamps.py)
+#ifdef VSIM_NB_STAMPS
+namespace vsim {
+__device__ unsigned long long g_nb_stamps[2048][32];
+}
+#define ATT_STAMP(i) \
+  if (threadIdx.x == 0) g_nb_stamps[1536 + blockIdx.x][4 + (i)] = __builtin_amdgcn_s_memrealtime()
+#endif
 #include "attn.hpp"
 #include "kern.hpp"
 #include "../../include/vsim_hip.h"
@@ -65,10 +75,9 @@ constexpr int c2_waves(int npw, bool fill) {
   while (p < npw) p += (!fill || w % 4 != 0) ? 1 : 0, ++w;
   return w;
 }
-template <int CB_, int DEPTH_, bool FILL_, int RING_ = 3>
+template <int CB_, int DEPTH_, bool FILL_>
 struct C2Shape {
   static constexpr int CB = CB_, CP = CB * 16, LD = CP + 4, NPW = CB / 2, DEPTH = DEPTH_;
-  static constexpr int RING = RING_;  // pair-term slots of the barrier-free hand-off (NbLds)
   static constexpr bool FILL = FILL_;
   static constexpr int THREADS = 64 * c2_waves(NPW, FILL);
   static constexpr int XP = (CB + 7) / 8;  // 1 KB factor pieces per chunk (8 blocks each)
@@ -315,10 +324,7 @@ __device__ __forceinline__ void nb_add_batch(float &acc, f32x4 (&cur)[BQ], const
 #pragma unroll
   for (int j = 0; j < BQ; ++j) cur[j] = nxt[j];
 }
-// VSIM_NB_STAMPS (a diagnostic build, tools/build_variant.sh): per-workgroup s_memtime sums of
-// where the barrier-free GEMVs' waves wait, read back by vsim_debug_nb_stamps
 #ifdef VSIM_NB_STAMPS
-__device__ unsigned long long g_nb_stamps[2048][32];
 #define NBS(...) __VA_ARGS__
 #else
 #define NBS(...)
@@ -335,11 +341,11 @@ constexpr int NB_RING = 3;
 constexpr unsigned NB_SPIN_MAX = 1u << 24;
 template <class S>
 struct NbLds {
-  float P[S::RING][32 * S::LD];
+  float P[NB_RING][32 * S::LD];
   uint4 RQ[S::DEPTH][S::NPW][64];
   float RD[S::DEPTH][S::NPW][64];
   float RX[S::DEPTH][S::NPW][64];
-  unsigned ready[S::RING];
+  unsigned ready[NB_RING];
   unsigned cons;
 };
 
@@ -347,16 +353,13 @@ __device__ __forceinline__ unsigned lds_load(const unsigned *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// One 32-row tile's pipeline run by the waves the caller assigns: role -1 = the consumer, 0 ..
-// NPW-1 = producer p, anything else returns.  The caller zeroes L.ready / L.cons and barriers
-// before any wave enters (chain32_nb_body does both for a workgroup running one tile).
-// SC1: the activation factors were written write-through by other workgroups of this launch.
-// CO: the plain-store epilogue stores write-through (sc1), for readers in the same launch.
-template <class S, bool SC1, bool CO = false>
-__device__ __forceinline__ void chain32_nb_role(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err, int role) {
-  constexpr int DEPTH = S::DEPTH, CB = S::CB, LD = S::LD, NPW = S::NPW, RING = S::RING;
+// SC1: the activation factors were written write-through by other workgroups of this launch
+template <class S, bool SC1>
+__device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err) {
+  constexpr int DEPTH = S::DEPTH, CB = S::CB, LD = S::LD, NPW = S::NPW;
   constexpr int WAIT_VM = waitcnt_vm(3 * (DEPTH - 1));  // chunk c landed, c+1 .. c+DEPTH-1 in flight
   static_assert(3 * (DEPTH - 1) < 64, "vmcnt immediate");
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   int ji = 0;
   while (ji < B.nj) {
@@ -364,15 +367,18 @@ __device__ __forceinline__ void chain32_nb_role(const GemvBatch &B, int t, NbLds
     t -= B.j[ji].w.tiles;
     ++ji;
   }
-  if (ji >= B.nj || role < -1 || role >= NPW) return;
+  if (ji >= B.nj) return;
   ji = __builtin_amdgcn_readfirstlane(ji);
-  role = __builtin_amdgcn_readfirstlane(role);
-  t = __builtin_amdgcn_readfirstlane(t);
   const int nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
+  if (threadIdx.x < NB_RING) L.ready[threadIdx.x] = 0;
+  if (threadIdx.x == 0) L.cons = 0;
+  __syncthreads();
+  if (S::FILL && wave > 0 && wave % 4 == 0) return;  // the consumer's SIMD is left to it
 
-  if (role >= 0) {
+  if (wave > 0) {
     // ------------------------------------------------------------- producer
-    const int p = role, r = lane & 31, hb = lane >> 5;
+    const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
+    if (p >= NPW) return;  // (a launch wider than this shape needs)
     const int o = 2 * p + hb;  // this lane's block within the chunk
     const uint8_t *qs = B.j[ji].w.qs + (size_t)t * nb * T32 * 16 + (size_t)r * 16;
     const float *dd = B.j[ji].w.d + (size_t)t * nb * T32 + r;
@@ -404,14 +410,14 @@ __device__ __forceinline__ void chain32_nb_role(const GemvBatch &B, int t, NbLds
       f0 = L.RX[slot][p][fx];
       f1 = L.RX[slot][p][fx + 16];
     };
-    // chunk k's pair terms into ring slot k % RING, then (lgkmcnt(0): the terms and the raw
+    // chunk k's pair terms into ring slot k % NB_RING, then (lgkmcnt(0): the terms and the raw
     // reads of chunk k+1 landed) the count, and the DMA of chunk k+1+DEPTH into the raw slot just read
     auto compute = [&](int k, float f0, float f1, const uint4 &qc, float dqc) {
-      const int slot = k % RING;
+      const int slot = k % NB_RING;
       NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
-      if (k >= RING) {
+      if (k >= NB_RING) {
         unsigned spins = 0;
-        while ((int)lds_load(&L.cons) < k - RING + 1) {
+        while ((int)lds_load(&L.cons) < k - NB_RING + 1) {
           __builtin_amdgcn_s_sleep(1);
           if (++spins == NB_SPIN_MAX) {
             if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -462,26 +468,20 @@ __device__ __forceinline__ void chain32_nb_role(const GemvBatch &B, int t, NbLds
   }
 
   // --------------------------------------------------------------- consumer (lanes 0-31)
-  // Batches of 8 float4 (32 adds) in four register sets: the reads of batch G+3 (G counted over
-  // the whole chain) go out with the adds of batch G, so a read has three batches (~100 adds)
-  // to land.  Batch G sits in set G % 4; one loop iteration covers CPI chunks, a whole number of
-  // rounds of the four sets, so the sets need no copies.  A chunk's count is compared before its
-  // first read (batch G with (G + 3) % NBQ == 0, LC chunks ahead of the one being added), having
-  // been read at the top of that chunk, so the poll costs no lgkmcnt(0) in the read pipeline.
+  // Batches of 8 float4 (32 adds) in four register sets: the reads of batch q+3 go out with the
+  // adds of batch q, so a read has three batches (~100 adds) to land.  Batch q of a chunk always
+  // sits in set q % 4 (8 batches per chunk), so the sets need no copies across chunks.
   float acc = 0.0f;
   const int lr = lane & 31;
   constexpr int NV = S::CP / 4, BQ = 8, NBQ = NV / BQ;  // float4 per chunk, per batch, batches
-  static_assert(NV % BQ == 0 && (NBQ % 4 == 0 || 4 % NBQ == 0), "batches tile the chunk in rounds of four sets");
-  constexpr int CPI = NBQ >= 4 ? 1 : 4 / NBQ;           // chunks per loop iteration
-  constexpr int QW = (NBQ - 3 % NBQ) % NBQ;              // the batch whose reads start a chunk
-  constexpr int LC = (QW + 3) / NBQ;                     // ... LC chunks ahead
-  auto need = [](int c) { return (unsigned)(NPW * (c / RING + 1)); };
+  static_assert(NV % BQ == 0 && NBQ % 4 == 0, "batches tile the chunk in whole rounds of four sets");
+  auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
   NBS(unsigned long long cw = 0;)
   auto wait_ready = [&](int c, unsigned have) {
     unsigned spins = 0;
     NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
     while (have < need(c)) {
-      have = lds_load(&L.ready[c % RING]);
+      have = lds_load(&L.ready[c % NB_RING]);
       if (++spins == NB_SPIN_MAX) {
         if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -492,37 +492,32 @@ __device__ __forceinline__ void chain32_nb_role(const GemvBatch &B, int t, NbLds
   };
   __builtin_amdgcn_s_setprio(3);
   NBS(const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();)
-#pragma unroll
-  for (int c = 0; c <= 2 / NBQ; ++c)  // the chunks of batches 0-2
-    if (c < nch) wait_ready(c, 0u);
+  wait_ready(0, 0u);
   f32x4 b0[BQ], b1[BQ], b2[BQ], b3[BQ];
   auto rd = [&](f32x4 (&d)[BQ], int c, int q) {  // batch q of chunk c (past the last chunk: harmless)
-    const f32x4 *src = (const f32x4 *)&L.P[c % RING][lr * LD] + q * BQ;
+    const f32x4 *src = (const f32x4 *)&L.P[c % NB_RING][lr * LD] + q * BQ;
 #pragma unroll
     for (int j = 0; j < BQ; ++j) d[j] = src[j];
   };
-  rd(b0, 0 / NBQ, 0 % NBQ);
-  rd(b1, 1 / NBQ, 1 % NBQ);
-  rd(b2, 2 / NBQ, 2 % NBQ);
-  for (int c0 = 0; c0 < nch; c0 += CPI) {
+  rd(b0, 0, 0);
+  rd(b1, 0, 1);
+  rd(b2, 0, 2);
+  for (int c = 0; c < nch; ++c) {
+    // the next chunk's count, read first: compared at batch NBQ-3 (before that chunk's first read),
+    // by when every read issued after it has had batches to land (a poll at the chunk's end
+    // drained the whole read pipeline: lgkmcnt(0) at its loop head)
+    const unsigned rdy = lds_load(&L.ready[(c + 1) % NB_RING]);
 #pragma unroll
-    for (int cc = 0; cc < CPI; ++cc) {
-      const int c = c0 + cc;
-      if (CPI > 1 && c >= nch) break;
-      const unsigned rdy = lds_load(&L.ready[(c + LC) % RING]);
-#pragma unroll
-      for (int q = 0; q < NBQ; ++q) {
-        const int gi = cc * NBQ + q;  // batch within the iteration: its set
-        const int qn = q + 3, cn = c + qn / NBQ, qr = qn % NBQ;
-        if (q == QW && cn < nch && rdy < need(cn)) wait_ready(cn, rdy);
-        asm volatile("" ::: "memory");
-        f32x4(&dst)[BQ] = ((gi + 3) % 4 == 0) ? b0 : ((gi + 3) % 4 == 1) ? b1 : ((gi + 3) % 4 == 2) ? b2 : b3;
-        rd(dst, cn, qr);
-        f32x4(&cur)[BQ] = (gi % 4 == 0) ? b0 : (gi % 4 == 1) ? b1 : (gi % 4 == 2) ? b2 : b3;
-        NB_ADDS8(acc, cur, 0);
-        if (q == NBQ - 1)  // the chunk's last reads landed (the adds waited for them): refill its slot
-          __hip_atomic_store(&L.cons, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+    for (int q = 0; q < NBQ; ++q) {
+      const int qn = q + 3, cn = qn < NBQ ? c : c + 1, qr = qn < NBQ ? qn : qn - NBQ;
+      if (qn == NBQ && c + 1 < nch && rdy < need(c + 1)) wait_ready(c + 1, rdy);
+      asm volatile("" ::: "memory");
+      f32x4(&dst)[BQ] = (qn % 4 == 0) ? b0 : (qn % 4 == 1) ? b1 : (qn % 4 == 2) ? b2 : b3;
+      rd(dst, cn, qr);
+      f32x4(&cur)[BQ] = (q % 4 == 0) ? b0 : (q % 4 == 1) ? b1 : (q % 4 == 2) ? b2 : b3;
+      NB_ADDS8(acc, cur, 0);
+      if (q == NBQ - 1)  // the chunk's last reads landed (the adds waited for them): refill its slot
+        __hip_atomic_store(&L.cons, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   __builtin_amdgcn_s_setprio(0);
@@ -543,74 +538,12 @@ __device__ __forceinline__ void chain32_nb_role(const GemvBatch &B, int t, NbLds
     float g = 0.0f;
     if (ok) {
       g = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
-      if (y) st_out<CO>(&y[row], g);
+      if (y) y[row] = g;
     }
-    quantize_half<CO>(g, lane, ok, B.j[ji].oq_qs + (size_t)t * 16, B.j[ji].oq_d + t, B.j[ji].oxd + (size_t)t * QK);
+    quantize_half(g, lane, ok, B.j[ji].oq_qs + (size_t)t * 16, B.j[ji].oq_d + t, B.j[ji].oxd + (size_t)t * QK);
   } else if (lane < 32 && row < rows) {
-    st_out<CO>(&y[row], bias ? acc + bias[row] : acc);
+    y[row] = bias ? acc + bias[row] : acc;
   }
-}
-
-// One 32-row tile per workgroup: wave 0 the consumer, the producers after it (S::FILL: none on
-// the consumer's SIMD, waves 4, 8, ... return).
-template <class S, bool SC1>
-__device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err) {
-  if (threadIdx.x < S::RING) L.ready[threadIdx.x] = 0;
-  if (threadIdx.x == 0) L.cons = 0;
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (S::FILL && wave > 0 && wave % 4 == 0) return;  // the consumer's SIMD is left to it
-  chain32_nb_role<S, SC1>(B, t, L, err, wave == 0 ? -1 : S::FILL ? wave - 1 - wave / 4 : wave - 1);
-}
-
-// Q, K and V tile t in one workgroup of the layer tail (k_layer_tail's QKV role): three
-// pipelines of chain32_nb_role with 4-block chunks, each a consumer on SIMD0 (waves 0, 4, 8) and
-// two producers, one on each of two of SIMD1-3 (waves 1,2 / 3,5 / 6,7; 9 and 10 return).  The
-// outputs are stored write-through; each consumer then drains its stores and counts itself in
-// *qdone (three per workgroup), which the attention heads wait for.
-// (4-block chunks: the consumer reads 1.5 chunks ahead, so four ring slots; LDS-DMA 5 chunks ahead)
-using C2Qkv = C2Shape<4, 5, false, 4>;
-struct QkvLds {
-  NbLds<C2Qkv> p[3];
-};
-__device__ __forceinline__ void qkv3_body(const GemvBatch &B, int t, QkvLds &L, unsigned *qdone, unsigned *err) {
-  if (threadIdx.x < 3 * C2Qkv::RING) L.p[threadIdx.x / C2Qkv::RING].ready[threadIdx.x % C2Qkv::RING] = 0;
-  if (threadIdx.x < 3) L.p[threadIdx.x].cons = 0;
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // wave -> (pipeline, role): consumers 0, 4, 8; producers (1, 2), (3, 5), (6, 7)
-  constexpr signed char PIPE[11] = {0, 0, 0, 1, 1, 1, 2, 2, 2, -1, -1};
-  constexpr signed char ROLE[11] = {-1, 0, 1, 0, -1, 1, 0, 1, -1, -2, -2};
-  if (wave >= 11 || PIPE[wave] < 0) return;
-  const int pi = __builtin_amdgcn_readfirstlane(PIPE[wave]), role = __builtin_amdgcn_readfirstlane(ROLE[wave]);
-  const int nt = B.j[0].w.tiles;
-  NbLds<C2Qkv> &P = pi == 0 ? L.p[0] : pi == 1 ? L.p[1] : L.p[2];
-  chain32_nb_role<C2Qkv, false, true>(B, pi * nt + t, P, err, role);
-  if (role == -1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through outputs landed
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(qdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// Two 32-row tiles per workgroup (k_gemv_duo): two chain32_nb_role pipelines of 8-block chunks,
-// consumers on SIMD0 (waves 0 and 4), four producers each (waves 1, 2, 3, 5 / 6, 7, 9, 10), one
-// workgroup per CU (150 KB of LDS).  For batches of K = n_embd (fc_in: 512 tiles, two per CU),
-// where k_gemv_solo's per-chunk barrier and 96-pair chunks cost the chain.
-using C2Duo = C2Shape<8, 4, false>;
-struct DuoLds {
-  NbLds<C2Duo> p[2];
-};
-__global__ void __launch_bounds__(C2Tail::THREADS, 1) k_gemv_duo(GemvBatch B, unsigned *err) {
-  __shared__ DuoLds L;
-  if (threadIdx.x < 2 * C2Duo::RING) L.p[threadIdx.x / C2Duo::RING].ready[threadIdx.x % C2Duo::RING] = 0;
-  if (threadIdx.x < 2) L.p[threadIdx.x].cons = 0;
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr signed char PIPE[11] = {0, 0, 0, 0, 1, 0, 1, 1, -1, 1, 1};
-  constexpr signed char ROLE[11] = {-1, 0, 1, 2, -1, 3, 0, 1, -2, 2, 3};
-  if (wave >= 11 || PIPE[wave] < 0) return;
-  const int pi = __builtin_amdgcn_readfirstlane(PIPE[wave]), role = __builtin_amdgcn_readfirstlane(ROLE[wave]);
-  chain32_nb_role<C2Duo, false>(B, 2 * blockIdx.x + pi, pi == 0 ? L.p[0] : L.p[1], err, role);
 }
 
 // ================================================================== fused layer tail
@@ -638,10 +571,10 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_gemv_duo(GemvBatch B, un
 // kept.  *done is zeroed by the layer's LayerNorm kernel.
 constexpr unsigned TAIL_SPIN_MAX = 1u << 22;
 struct TailJob {
-  GemvBatch f, o, q;
+  GemvBatch f, o;
   AttnJob a;
-  unsigned *done, *qdone, *err;
-  int nf, nq;
+  unsigned *done, *err;
+  int nf;
 };
 
 template <int NBM>
@@ -649,12 +582,11 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   __shared__ union {
     C2Lds<C2Tail> g;
     NbLds<C2Tail> n;
-    QkvLds q;
     float a[sizeof(C2Lds<C2Tail>) / sizeof(float)];
   } L;
   int b = blockIdx.x;
-  // (VSIM_NB_STAMPS: s_memrealtime timeline per workgroup in rows 1536.. : start, then the role's
-  // marks; tools/nb_stamps.py)
+  // (VSIM_NB_STAMPS: s_memrealtime timeline per workgroup in rows 1536.. : start, the role's
+  // marks, end; tools/nb_stamps.py)
   NBS(unsigned long long *tl = g_nb_stamps[1536 + blockIdx.x];
       if (threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();)
   if (b < T.nf) {
@@ -666,34 +598,10 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
     return;
   }
   b -= T.nf;
-  if (b < T.nq) {
-    qkv3_body(T.q, b, L.q, T.qdone, T.err);
-    NBS(if ((threadIdx.x & 255) == 0 && threadIdx.x < 64 * 9) tl[1 + threadIdx.x / 256] = __builtin_amdgcn_s_memrealtime();)
-    return;
-  }
-  b -= T.nq;
   const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
-  auto wait_count = [&](const unsigned *cnt, unsigned target) {
-    if (threadIdx.x == 0) {
-      unsigned spins = 0;
-      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(8);
-        if (++spins == TAIL_SPIN_MAX) {
-          if (T.err) __hip_atomic_fetch_add(T.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-  };
   if (b < na) {
-    if (T.nq > 0) {  // Q, K, V come from this launch's QKV workgroups: their count, then sc1 loads
-      wait_count(T.qdone, 3u * T.nq);
-      NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
-      attn_body<C2Tail::THREADS, true, true>(T.a, b, L.a);
-    } else {
-      attn_body<C2Tail::THREADS, true>(T.a, b, L.a);
-    }
+    attn_body<C2Tail::THREADS, true>(T.a, b, L.a);
+    NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through output stores landed
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -701,7 +609,17 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
     return;
   }
   b -= na;
-  wait_count(T.done, na);
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)na) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins == TAIL_SPIN_MAX) {
+        if (T.err) __hip_atomic_fetch_add(T.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
   NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
   if constexpr (NBM & 2)
     chain32_nb_body<C2Tail, true>(T.o, b, L.n, T.err);
@@ -710,31 +628,22 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
 }
 
-// q (optional, q.nj == 3 with equal tile counts, or q.nj == 0): Q, K, V computed inside the
-// launch by qkv3_body workgroups (placed after fc_out's tiles), counted in done[64]
-int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const GemvBatch &q, const AttnJob &a, unsigned *done,
-                      int n_ctx, hipStream_t s) {
+int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
+                      hipStream_t s) {
   const int S = a.nsplit > 1 ? a.nsplit : 1;
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
       (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds<C2Tail>)) {
     set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
     return VSIM_EINVAL;
   }
-  if (q.nj != 0 && (q.nj != 3 || q.j[1].w.tiles != q.j[0].w.tiles || q.j[2].w.tiles != q.j[0].w.tiles)) {
-    set_error("layer tail: the QKV role takes three jobs of equal row counts");
-    return VSIM_EINVAL;
-  }
   TailJob T;
   T.f = f;
   T.o = o;
-  T.q = q;
   T.a = a;
   T.done = done;
-  T.qdone = done + 64;
   T.err = spin_error_counter();
   T.nf = 0;
   for (int i = 0; i < f.nj; ++i) T.nf += f.j[i].w.tiles;
-  T.nq = q.nj ? q.j[0].w.tiles : 0;
   int no = 0;
   for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;
   // one workgroup per CU (fc_out's consumer keeps its SIMD): the static LDS is above half the
@@ -748,7 +657,7 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const GemvBatch &q
     const char *e = getenv("VSIM_TAIL_NB");
     return e ? atoi(e) & 3 : 3;
   }();
-  const dim3 grid(T.nf + T.nq + a.H * S + no), blk(C2Tail::THREADS);
+  const dim3 grid(T.nf + a.H * S + no), blk(C2Tail::THREADS);
   if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, 8192, s, T);
   if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, 8192, s, T);
   if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, 8192, s, T);
@@ -1183,13 +1092,8 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     const char *e = getenv("VSIM_SOLO_NB");
     return e ? atoi(e) : 0;
   }();
-  static const bool duo = [] {
-    const char *e = getenv("VSIM_GEMV_DUO");
-    return e && atoi(e) != 0;
-  }();
-  if (gemv_chain_solo(B) && duo) {
-    hipLaunchKernelGGL(k_gemv_duo, dim3((tiles + 1) / 2), dim3(C2Tail::THREADS), 0, s, B, spin_error_counter());
-  } else if (gemv_chain_solo(B) && solo_nb == 1) {
+
+  if (gemv_chain_solo(B) && solo_nb == 1) {
     hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)),
                        dim3(64 * SoloShape<SOLO_CB, 1>::WAVES), 0, s, B, spin_error_counter());
   } else if (gemv_chain_solo(B) && solo_nb == 2) {

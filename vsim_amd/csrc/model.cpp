@@ -950,7 +950,20 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.n_rot = bloom ? 0 : m->hp.n_rot;
     A.style = gptj ? 1 : 0;
     A.n_ctx = m->n_ctx;
+    // each head over two workgroups (its KQV columns halved; the scores computed by both): r05,
+    // 248-token lines 608.9 / 612.5 vs 606.9 / 610.8 tok/s unsplit, 602.6 / 601.3 at four
+    // (profiles/r05_tail_variants_ab.txt).  The largest split <= VSIM_ATT_SPLIT (default 2)
+    // whose column parts are whole 32-blocks.
+    static const int att_split = [] {
+      const char *e = getenv("VSIM_ATT_SPLIT");
+      return e ? atoi(e) : 2;
+    }();
     A.nsplit = 1;
+    for (int sp = att_split; sp > 1; --sp)
+      if (d % sp == 0 && (d / sp) % QK == 0) {
+        A.nsplit = sp;
+        break;
+      }
     A.scale = m->attn_scale != 0.0f ? m->attn_scale : scale;
     A.kqv_nth = m->kqv_nth;
     A.alibi = bloom ? m->alibi : nullptr;
@@ -998,7 +1011,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       if (tail) {
         GemvBatch none{};
         ev = prof_begin(m);
-        RC(launch_layer_tail(none, Bo, none, A, m->tail_done, m->n_ctx, s));
+        RC(launch_layer_tail(none, Bo, A, m->tail_done, m->n_ctx, s));
         prof_end(m, ev, "k_layer_tail (attention + out-proj)", w4_algo_bytes(Bo.j[0].w) + kv_bytes);
         ++nk;
       } else {
@@ -1051,37 +1064,24 @@ int enqueue_decode(vsim_model *m, int &nk) {
     prof_end(m, ev, "k_ln_quant", ln_bytes(gptj ? 1 : 2, pending));
     ++nk;
     if (pending) cur ^= 1;
-    // 2. fc_in (+bias, GELU, requantize), with Q, K, V unless they join the tail (step 3)
-    // r05: Q, K and V as k_layer_tail's QKV role (three tiles per workgroup on the CUs beside
-    // fc_out's), so the solo launch holds fc_in's 64-row groups alone, one per CU, instead of
-    // two per CU on most of them; VSIM_TAIL_QKV=0 keeps them in the solo batch (A/B).
-    static const bool qkv_in_tail = [] {
-      const char *e = getenv("VSIM_TAIL_QKV");
-      return !e || atoi(e) != 0;
-    }();
-    const bool tq = tail && qkv_in_tail;
-    GemvBatch B{}, Bq{};
-    B.nj = tq ? 1 : 4;
+    // 2. {fc_in (+bias, GELU, requantize), Q, K, V}
+    GemvBatch B{};
+    B.nj = 4;
     job(B, 0, L.wfc, F, E, gptj ? m->xd1 : m->xd2, gptj ? q1 : q2, gptj ? d1 : d2, L.bfc, nullptr);
     B.j[0].epi = EPI_GELU_Q;
     B.j[0].gelu_tab = tab.gelu_f16;
     B.j[0].oq_qs = q3;
     B.j[0].oq_d = d3;
     B.j[0].oxd = m->xd3;
-    GemvBatch &Bk = tq ? Bq : B;
-    const int k0 = tq ? 0 : 1;
-    Bk.nj = k0 + 3;
-    job(Bk, k0 + 0, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
-    job(Bk, k0 + 1, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
-    job(Bk, k0 + 2, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
+    job(B, 1, L.wq, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bq, m->Qb);
+    job(B, 2, L.wk, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bk, m->Kb);
+    job(B, 3, L.wv, E, E, m->xd1, q1, d1, gptj ? nullptr : L.bv, m->Vb);
     ev = prof_begin(m);
     RC(launch_gemv_epi(B, m->mode, s));
-    prof_end(m, ev, m->mode != VSIM_MODE_EXACT ? "k_gemv_fast_epi (fc_in, Q, K, V)"
-                    : tq                       ? "k_gemv_solo (fc_in)"
-                                               : "k_gemv_solo (fc_in, Q, K, V)",
-             w4_algo_bytes(B.j[0].w) + (tq ? 0.0 : 3 * w4_algo_bytes(B.j[1].w)));
+    prof_end(m, ev, m->mode == VSIM_MODE_EXACT ? "k_gemv_solo (fc_in, Q, K, V)" : "k_gemv_fast_epi (fc_in, Q, K, V)",
+             w4_algo_bytes(B.j[0].w) + 3 * w4_algo_bytes(B.j[1].w));
     ++nk;
-    // 3. attention for the new token (attn.hpp), fc_out and the out-projection (+ Q, K, V)
+    // 3. attention for the new token (attn.hpp), fc_out and the out-projection
     const AttnJob A = attn_job(loff);
     GemvBatch Bf{}, Bo{};
     Bf.nj = 1;
@@ -1090,9 +1090,9 @@ int enqueue_decode(vsim_model *m, int &nk) {
     job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
     if (tail) {
       ev = prof_begin(m);
-      RC(launch_layer_tail(Bf, Bo, Bq, A, m->tail_done, m->n_ctx, s));
-      prof_end(m, ev, tq ? "k_layer_tail (fc_out + Q, K, V + attention + out-proj)" : "k_layer_tail (fc_out + attention + out-proj)",
-               w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + (tq ? 3 * w4_algo_bytes(Bq.j[0].w) : 0.0) + kv_bytes);
+      RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
+      prof_end(m, ev, "k_layer_tail (fc_out + attention + out-proj)",
+               w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + kv_bytes);
       ++nk;
     } else {
       ev = prof_begin(m);
