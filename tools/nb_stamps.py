@@ -1,8 +1,8 @@
 """Where the barrier-free chain GEMVs wait (r05 diagnostic): GPT-J-6B exact decode on the
 VSIM_NB_STAMPS build (tools/build_variant.sh nbstamps Makefile 's/-fno-slp-vectorize$/& -DVSIM_NB_STAMPS/'),
-VSIM_TAIL_NB=3 VSIM_SOLO_NB=1, then the per-workgroup s_memtime sums of the last launches:
-the last layer's tail (fc_out tiles 0..127, out-projection tiles after the 16 heads) and the
-last per-layer k_gemv_solo_nb batch.  Prints medians per chunk (cycles of the shader clock)."""
+then the per-workgroup s_memtime sums of the last layer's tail (fc_out tiles 0..127, the
+out-projection tiles after the heads): medians per chunk (cycles of the shader clock), and the
+tail's s_memrealtime timeline by role."""
 import ctypes
 import os
 import sys
@@ -45,16 +45,12 @@ def role(name, rows, nprod, off):
 
 role("tail fc_out tiles", np.arange(0, 128), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
 role("tail out-proj tiles", np.arange(144 + (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0), 272 + (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0)), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
-nsolo = 0  # (k_gemv_solo_nb is not in the r05 decode path)
-if nsolo:
-    role("k_gemv_solo_nb batch (fc_in, Q, K, V), first 64-row half", np.arange(1024, 1024 + nsolo), 6,
-         [("lgkm wait", 4), ("slot wait", 10), ("compute", 16)])
 
 # the last tail's timeline (s_memrealtime, 100 MHz; rows 1536 + workgroup): fc_out tiles, QKV
 # workgroups (three consumers' ends), heads (count reached, end), out-projection (count, end)
 nf, nq = 128, (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0)
 na, no = 16, 128
-tl = buf[1536:1536 + nf + nq + na + no, :4].astype(np.int64)
+tl = buf[1536:1536 + nf + nq + na + no, :8].astype(np.int64)
 t0 = tl[:, 0].min()
 us = lambda v: (v - t0) / 100.0  # noqa: E731
 
@@ -66,7 +62,7 @@ def tlrow(name, rows, cols):
 
 
 print("tail timeline (us from the first workgroup's start):")
-tlrow("fc_out", np.arange(0, nf), [("end", 2)])
+tlrow("fc_out", np.arange(0, nf), [("dma issued", 4), ("chunk 0 landed", 5), ("chunk 1 landed", 6), ("chunk 0 computed", 7), ("chunk 0 ready", 3), ("end", 2)])
 if nq:
     tlrow("QKV", np.arange(nf, nf + nq), [("Q end", 1), ("K end", 2), ("V end", 3)])
 tlrow("heads", np.arange(nf + nq, nf + nq + na), [("attn", 1), ("end", 2)])
@@ -77,3 +73,12 @@ ph = buf[1536 + nf + nq:1536 + nf + nq + na, 4:8].astype(np.int64)
 print("heads phases (us, medians): setup+RoPE %.2f  KQ %.2f  softmax %.2f  KQV %.2f  quantize %.2f" % (
     np.median(ph[:, 0] - hr[:, 0]) / 100, np.median(ph[:, 1] - ph[:, 0]) / 100, np.median(ph[:, 2] - ph[:, 1]) / 100,
     np.median(ph[:, 3] - ph[:, 2]) / 100, np.median(hr[:, 1] - ph[:, 3]) / 100))
+# the slowest fc_out tiles (end time, consumer wait per chunk, its producers' slot wait)
+fo = tl[:nf]
+order = np.argsort(-fo[:, 2])
+print("slowest fc_out tiles (index, XCD = index % 8, end us, consumer wait/chunk, producer slot wait/chunk, dma wait/chunk):")
+for i in order[:8]:
+    b = buf[i]
+    nchk = max(int(b[3]), 1)
+    print(f"  {i:4d} {i % 8} {us(fo[i, 2]):6.2f} {b[2] / nchk:7.0f} {np.median(b[12:20]) / nchk:7.0f} {np.median(b[4:12]) / nchk:7.0f}")
+print("end-time quartiles:", np.percentile(us(fo[:, 2]), [0, 25, 50, 75, 100]).round(2))

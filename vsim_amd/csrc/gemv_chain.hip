@@ -75,9 +75,12 @@ constexpr int c2_waves(int npw, bool fill) {
   while (p < npw) p += (!fill || w % 4 != 0) ? 1 : 0, ++w;
   return w;
 }
-template <int CB_, int DEPTH_, bool FILL_>
+template <int CB_, int DEPTH_, bool FILL_, int PAD_ = 4>
 struct C2Shape {
-  static constexpr int CB = CB_, CP = CB * 16, LD = CP + 4, NPW = CB / 2, DEPTH = DEPTH_;
+  // PAD: row pad of the pair-term ring in floats (LD = CP + PAD); 8 for the pair-lane consumer
+  // (chain32_nb_body): rows 8 banks apart, so the 32-byte row pieces of one 16-byte read per lane
+  // pair and the producers' 16-byte stores are both conflict-free
+  static constexpr int CB = CB_, CP = CB * 16, LD = CP + PAD_, NPW = CB / 2, DEPTH = DEPTH_;
   static constexpr bool FILL = FILL_;
   static constexpr int THREADS = 64 * c2_waves(NPW, FILL);
   static constexpr int XP = (CB + 7) / 8;  // 1 KB factor pieces per chunk (8 blocks each)
@@ -93,7 +96,7 @@ constexpr int C2_RING = 3, C2_WIN = 16;
 // the 8-block shape with wave 4 producing beside the consumer 36.0-36.3 (581.4-582.7); 3 chunks
 // ahead 34.8-34.9 (profiles/r04_tail_consumer_ab.txt)
 using C2Gemv = C2Shape<8, 4, false>;
-using C2Tail = C2Shape<16, 4, true>;
+using C2Tail = C2Shape<16, 2, true, 8>;
 
 template <class S>
 struct C2Lds {
@@ -314,30 +317,30 @@ __global__ void __launch_bounds__(C2Gemv::THREADS, 2) k_gemv_chain32(GemvBatch B
                  "v"(a[o + 1].z), "v"(a[o + 1].w), "v"(a[o + 2].x), "v"(a[o + 2].y), "v"(a[o + 2].z),            \
                  "v"(a[o + 2].w), "v"(a[o + 3].x), "v"(a[o + 3].y), "v"(a[o + 3].z), "v"(a[o + 3].w)             \
                : "memory")
-// acc += the BQ float4 of cur in order (BQ a multiple of 4), then cur = nxt
-template <int BQ>
-__device__ __forceinline__ void nb_add_batch(float &acc, f32x4 (&cur)[BQ], const f32x4 (&nxt)[BQ]) {
-  static_assert(BQ % 4 == 0, "batches of 4 float4");
-#pragma unroll
-  for (int o = 0; o + 8 <= BQ; o += 8) NB_ADDS8(acc, cur, o);
-  if constexpr (BQ % 8 == 4) NB_ADDS4(acc, cur, BQ - 4);
-#pragma unroll
-  for (int j = 0; j < BQ; ++j) cur[j] = nxt[j];
-}
+// The pair-lane form (chain32_nb_body's consumer): lanes 2r and 2r+1 hold terms 8i..8i+3 and
+// 8i+4..8i+7 of row r in float4 a[o+i]; lane 2r adds its own four, then its partner's four through
+// a DPP quad_perm source (lane 2r+1 runs a chain of no use).  One 16-byte read then brings 8 terms
+// of a row instead of 4 (r05: tools/cons_lat5.hip, the dependent DPP add costs what the plain one
+// does, 4.63 cycles; a consumer loop with 4x fewer reads ran 4.96 vs 5.53 cycles per add alone
+// and 5.48 vs 8.14 beside eight busy producers).
+#define NB_DP(i) "v_add_f32_dpp %0, %" #i ", %0 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf\n\t"
+#define NB_PAIR(a, b, c, d) NB_A4(a) NB_A4(b) NB_A4(c) NB_A4(d) NB_DP(a) NB_DP(b) NB_DP(c) NB_DP(d)
+#define NB_ADDS4P(acc, a, o)                                                                                     \
+  asm volatile(NB_PAIR(1, 2, 3, 4) NB_PAIR(5, 6, 7, 8) NB_PAIR(9, 10, 11, 12) NB_PAIR(13, 14, 15, 16)              \
+               : "+v"(acc)                                                                                       \
+               : "v"(a[o].x), "v"(a[o].y), "v"(a[o].z), "v"(a[o].w), "v"(a[o + 1].x), "v"(a[o + 1].y),           \
+                 "v"(a[o + 1].z), "v"(a[o + 1].w), "v"(a[o + 2].x), "v"(a[o + 2].y), "v"(a[o + 2].z),            \
+                 "v"(a[o + 2].w), "v"(a[o + 3].x), "v"(a[o + 3].y), "v"(a[o + 3].z), "v"(a[o + 3].w)             \
+               : "memory")
 #ifdef VSIM_NB_STAMPS
 #define NBS(...) __VA_ARGS__
 #else
 #define NBS(...)
 #endif
-constexpr int NB_RING = 3;
-// float4 per consumer batch (the reads of the next batch are in flight during this one's adds;
-// lgkmcnt counts at most 15, so a batch stays below that with the counter read and the store)
-#ifndef NB_TAIL_BQ
-#define NB_TAIL_BQ 8
+#ifndef NB_RING_N  // pair-term ring slots of the barrier-free GEMVs (A/B builds override)
+#define NB_RING_N 4
 #endif
-#ifndef NB_SOLO_BQ
-#define NB_SOLO_BQ 12
-#endif
+constexpr int NB_RING = NB_RING_N;
 constexpr unsigned NB_SPIN_MAX = 1u << 24;
 template <class S>
 struct NbLds {
@@ -467,55 +470,72 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
     return;
   }
 
-  // --------------------------------------------------------------- consumer (lanes 0-31)
-  // Batches of 8 float4 (32 adds) in four register sets: the reads of batch q+3 go out with the
-  // adds of batch q, so a read has three batches (~100 adds) to land.  Batch q of a chunk always
-  // sits in set q % 4 (8 batches per chunk), so the sets need no copies across chunks.
+  // --------------------------------------------------------------- consumer (row r: lane 2r)
+  // Batches of 4 reads (32 terms of each row, NB_ADDS4P) in four register sets: the reads of batch
+  // q+3 go out with the adds of batch q, so a read has three batches (~100 adds) to land, and at
+  // most 13 LDS reads are in flight (lgkmcnt counts 15: every wait is exact).  Batch q of a chunk
+  // always sits in set q % 4 (8 batches per chunk), so the sets need no copies across chunks.
   float acc = 0.0f;
-  const int lr = lane & 31;
-  constexpr int NV = S::CP / 4, BQ = 8, NBQ = NV / BQ;  // float4 per chunk, per batch, batches
+  const int lr = lane >> 1, lk = lane & 1;
+  constexpr int NV = S::CP / 8, BQ = 4, NBQ = NV / BQ;  // 8-term reads per chunk and row, per batch, batches
   static_assert(NV % BQ == 0 && NBQ % 4 == 0, "batches tile the chunk in whole rounds of four sets");
   auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
   NBS(unsigned long long cw = 0;)
+  // (the re-poll is asm: a C++ loop of LDS loads made the compiler drain every read in flight
+  // where its path joins the fast one, once per chunk)
   auto wait_ready = [&](int c, unsigned have) {
-    unsigned spins = 0;
     NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
-    while (have < need(c)) {
-      have = lds_load(&L.ready[c % NB_RING]);
-      if (++spins == NB_SPIN_MAX) {
-        if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+    if (have < need(c)) {
+      unsigned spins = 0, h;
+      asm volatile(
+          "1:\n\t"
+          "ds_read_b32 %0, %2\n\t"
+          "s_waitcnt lgkmcnt(0)\n\t"
+          "v_cmp_lt_u32 vcc, %0, %3\n\t"
+          "s_cbranch_vccz 2f\n\t"
+          "s_add_u32 %1, %1, 1\n\t"
+          "s_cmp_lt_u32 %1, %4\n\t"
+          "s_cbranch_scc1 1b\n\t"
+          "2:"
+          : "=&v"(h), "+s"(spins)
+          : "v"(lds_addr(&L.ready[c % NB_RING])), "s"(need(c)), "s"(NB_SPIN_MAX)
+          : "vcc", "scc", "memory");
+      if (spins >= NB_SPIN_MAX && err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     NBS(cw += __builtin_amdgcn_s_memtime() - t0;)
-    asm volatile("" ::: "memory");
   };
   __builtin_amdgcn_s_setprio(3);
   NBS(const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();)
   wait_ready(0, 0u);
   f32x4 b0[BQ], b1[BQ], b2[BQ], b3[BQ];
   auto rd = [&](f32x4 (&d)[BQ], int c, int q) {  // batch q of chunk c (past the last chunk: harmless)
-    const f32x4 *src = (const f32x4 *)&L.P[c % NB_RING][lr * LD] + q * BQ;
+    const f32x4 *src = (const f32x4 *)&L.P[c % NB_RING][lr * LD] + 2 * q * BQ + lk;
 #pragma unroll
-    for (int j = 0; j < BQ; ++j) d[j] = src[j];
+    for (int j = 0; j < BQ; ++j) d[j] = src[2 * j];
   };
   rd(b0, 0, 0);
   rd(b1, 0, 1);
   rd(b2, 0, 2);
   for (int c = 0; c < nch; ++c) {
-    // the next chunk's count, read first: compared at batch NBQ-3 (before that chunk's first read),
-    // by when every read issued after it has had batches to land (a poll at the chunk's end
-    // drained the whole read pipeline: lgkmcnt(0) at its loop head)
-    const unsigned rdy = lds_load(&L.ready[(c + 1) % NB_RING]);
+    // the next chunk's count is read after batch NBQ-6's adds (behind the reads of batch NBQ-3,
+    // so it lands with them) and compared at batch NBQ-3, before that chunk's first read; r05: read
+    // at the chunk's top instead, it was often short by the chunk's last producers, and the
+    // re-poll cost ~180 cycles a chunk (a poll at the chunk's end drained the read pipeline)
+    unsigned rdy = 0;
 #pragma unroll
     for (int q = 0; q < NBQ; ++q) {
       const int qn = q + 3, cn = qn < NBQ ? c : c + 1, qr = qn < NBQ ? qn : qn - NBQ;
-      if (qn == NBQ && c + 1 < nch && rdy < need(c + 1)) wait_ready(c + 1, rdy);
+      if (q == NBQ - 5) rdy = lds_load(&L.ready[(c + 1) % NB_RING]);
+      if (qn == NBQ && c + 1 < nch) {
+        unsigned r = rdy;
+        asm volatile("" : "+v"(r));  // compared here, not where it was read
+        wait_ready(c + 1, r);
+      }
       asm volatile("" ::: "memory");
       f32x4(&dst)[BQ] = (qn % 4 == 0) ? b0 : (qn % 4 == 1) ? b1 : (qn % 4 == 2) ? b2 : b3;
       rd(dst, cn, qr);
       f32x4(&cur)[BQ] = (q % 4 == 0) ? b0 : (q % 4 == 1) ? b1 : (q % 4 == 2) ? b2 : b3;
-      NB_ADDS8(acc, cur, 0);
+      NB_ADDS4P(acc, cur, 0);
       if (q == NBQ - 1)  // the chunk's last reads landed (the adds waited for them): refill its slot
         __hip_atomic_store(&L.cons, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -527,9 +547,10 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
     g_nb_stamps[blockIdx.x][2] = cw;
     g_nb_stamps[blockIdx.x][3] = nch;
   })
+  acc = __shfl(acc, (2 * lane) & 63);  // row r's sum from lane 2r to lane r (lanes 32-63: copies)
 
   // ----------------------------------------------------------------- epilogue
-  const int row = t * T32 + lr;
+  const int row = t * T32 + (lane & 31);
   const int rows = B.j[ji].w.rows;
   const float *bias = B.j[ji].bias;
   float *y = B.j[ji].y;
@@ -658,10 +679,12 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
     return e ? atoi(e) & 3 : 3;
   }();
   const dim3 grid(T.nf + a.H * S + no), blk(C2Tail::THREADS);
-  if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, 8192, s, T);
-  if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, 8192, s, T);
-  if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, 8192, s, T);
-  if (nbm == 3) hipLaunchKernelGGL(k_layer_tail<3>, grid, blk, 8192, s, T);
+  constexpr size_t lds_static = sizeof(NbLds<C2Tail>) > sizeof(C2Lds<C2Tail>) ? sizeof(NbLds<C2Tail>) : sizeof(C2Lds<C2Tail>);
+  constexpr size_t pad = lds_static > 80 * 1024 ? 0 : 81 * 1024 - lds_static;  // (one workgroup per CU)
+  if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, pad, s, T);
+  if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, pad, s, T);
+  if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, pad, s, T);
+  if (nbm == 3) hipLaunchKernelGGL(k_layer_tail<3>, grid, blk, pad, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
@@ -852,211 +875,6 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   __builtin_amdgcn_s_setprio(0);
 }
 
-// ---------------------------------------------------------------- 64-row, barrier-free
-// k_gemv_solo's shape and arithmetic with the chain32_nb_body hand-off in place of the per-chunk
-// barrier: each producer counts its block of chunk k into ready[k % NB_RING] once its stores
-// landed (at the top of step k+1, whose lgkmcnt(0) also covers its scalar-loaded factors), and
-// waits for the consumer's count before overwriting a slot; the consumer reads in batches of 8.
-// r02's barrier-free variant (per-slot counters too) lost to the barrier with the one-read-per-4-
-// adds consumer; r05 measures it again with the batched consumer.
-// CONS = 2: 128 rows, the two consumers (waves 0 and 4) on one SIMD, twelve producers on the other
-// three; each 64-row half has its own ready counters and consumer count.
-template <int CB, int PF, int CONS>
-__device__ __forceinline__ void solo_nb_body(const GemvBatch &B, int g, float (*P)[SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD],
-                                             unsigned (*ready)[NB_RING], unsigned *consw, unsigned *err) {
-  using S = SoloShape<CB, CONS>;
-  constexpr int LD = S::LD, TPG = 2 * CONS;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  int ji = 0;
-  while (ji < B.nj) {
-    const int ng = (B.j[ji].w.tiles + TPG - 1) / TPG;
-    if (g < ng) break;
-    g -= ng;
-    ++ji;
-  }
-  if (ji >= B.nj) return;
-  ji = __builtin_amdgcn_readfirstlane(ji);
-  g = __builtin_amdgcn_readfirstlane(g);
-  const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
-  if (threadIdx.x < CONS * NB_RING) (&ready[0][0])[threadIdx.x] = 0;
-  if (threadIdx.x < CONS) consw[threadIdx.x] = 0;
-  __syncthreads();
-  if ((wave & 3) == 0 && (wave >> 2) >= CONS) return;  // the consumers' SIMD is left to them
-
-  if ((wave & 3) != 0) {
-    // ------------------------------------------------------------- producer
-    const int pi = wave - 1 - (wave >> 2);  // waves 1,2,3,5,6,7,9,... -> 0,1,2,...
-    const int o = pi % CB, c = pi / CB;     // block of the chunk, the 64-row half (consumer) served
-    const int h = lane >> 5, r = lane & 31;
-    const int tile = TPG * g + 2 * c + h;
-    const bool tile_ok = tile < tiles;
-    const int tl = tile_ok ? tile : tiles - 1;
-    const uint8_t *qs = B.j[ji].w.qs + ((size_t)tl * nb * T32 + r) * 16;
-    const float *dd = B.j[ji].w.d + (size_t)tl * nb * T32 + r;
-    const float *xg = B.j[ji].xd;
-    auto ld = [&](int c, u32x4 &qv, float &dv) {
-      const int b = min(c * CB + o, nb - 1);
-      qv = __builtin_nontemporal_load((gu32x4 *)(qs + (size_t)b * (T32 * 16)));
-      dv = __builtin_nontemporal_load((gfloat *)(dd + (size_t)b * T32));
-    };
-    auto ldx = [&](int c, f32x2 *xv) {
-      const int b = min(c * CB + o, nb - 1);
-      const sfloat *xp = (const sfloat *)(xg + (size_t)b * QK);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        xv[i].x = xp[2 * i];
-        xv[i].y = xp[2 * i + 1];
-      }
-    };
-    auto signal = [&](int k) {  // chunk k's terms are in LDS (after an lgkmcnt(0))
-      if (lane == 0) __hip_atomic_fetch_add(&ready[c][k % NB_RING], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    NBS(unsigned long long sw_f = 0, sw_slot = 0, sw_comp = 0;)
-    auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
-      ld(k + PF, qn, dqn);
-      NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this chunk's factors, the last chunk's stores
-      __builtin_amdgcn_sched_barrier(0);
-      NBS(const unsigned long long t1 = __builtin_amdgcn_s_memtime(); sw_f += t1 - t0;)
-      if (k > 0) signal(k - 1);
-      ldx(k + 1, xn);
-      __builtin_amdgcn_sched_barrier(0);
-      if (k >= NB_RING) {  // slot k % NB_RING: the consumer is done with chunk k - NB_RING
-        unsigned spins = 0;
-        while ((int)lds_load(&consw[c]) < k - NB_RING + 1) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins == NB_SPIN_MAX) {
-            if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-        asm volatile("" ::: "memory");
-      }
-      NBS(const unsigned long long t2 = __builtin_amdgcn_s_memtime(); sw_slot += t2 - t1;)
-      const float dv = tile_ok && k * CB + o < nb ? dqc : 0.0f;
-      const float dl = 512.0f * dv, ml = -8.0f * dv;
-      float dh, mh;
-      asm("v_mov_b32 %0, %1" : "=v"(dh) : "v"(dl));  // (as in solo_body)
-      asm("v_mov_b32 %0, %1" : "=v"(mh) : "v"(ml));
-      const f32x2 d2 = {dl, dh}, m2 = {ml, mh};
-      float *dst = &P[k % NB_RING][(64 * c + lane) * LD + o * 16];
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) {
-        float p4[4];
-        pair_terms4_x(qc[wv], d2, m2, xc + 4 * wv, p4);
-        *(float4 *)(dst + 4 * wv) = make_float4(p4[0], p4[1], p4[2], p4[3]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      NBS(sw_comp += __builtin_amdgcn_s_memtime() - t2;)
-    };
-    u32x4 q[PF + 1];
-    float e[PF + 1];
-#pragma unroll
-    for (int c = 0; c < PF; ++c) ld(c, q[c], e[c]);
-    f32x2 xa[16], xb[16];
-    ldx(0, xa);
-    static_assert((PF + 1) % 2 == 0, "two factor sets alternate");
-    for (int k = 0; k < nch; k += PF + 1) {
-#pragma unroll
-      for (int u = 0; u < PF + 1; u += 2) {
-        if (k + u < nch) step(k + u, xa, xb, q[u], e[u], q[(u + PF) % (PF + 1)], e[(u + PF) % (PF + 1)]);
-        if (k + u + 1 < nch) step(k + u + 1, xb, xa, q[u + 1], e[u + 1], q[u % (PF + 1)], e[u % (PF + 1)]);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    signal(nch - 1);
-    NBS(if (lane == 0 && B.nj > 1 && c == 0) {  // (rows 1024.. : the tail owns 0..)
-      g_nb_stamps[1024 + blockIdx.x][4 + o] = sw_f;
-      g_nb_stamps[1024 + blockIdx.x][10 + o] = sw_slot;
-      g_nb_stamps[1024 + blockIdx.x][16 + o] = sw_comp;
-      g_nb_stamps[1024 + blockIdx.x][22 + o] = __builtin_amdgcn_s_memtime();
-    })
-    return;
-  }
-
-  // --------------------------------------------------------------- consumer (64 rows each)
-  float acc = 0.0f;
-  const int cw_i = wave >> 2, crow = 64 * cw_i + lane;  // this consumer's half, its row in the group
-  constexpr int NV = S::CP / 4, BQ = NB_SOLO_BQ, NBQ = NV / BQ, NPW = CB;
-  static_assert(NV % BQ == 0 && NBQ >= 2, "batches tile the chunk");
-  auto need = [](int c) { return (unsigned)(NPW * (c / NB_RING + 1)); };
-  NBS(unsigned long long cw = 0;)
-  auto wait_ready = [&](int c, unsigned have) {
-    unsigned spins = 0;
-    NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
-    while (have < need(c)) {
-      have = lds_load(&ready[cw_i][c % NB_RING]);
-      if (++spins == NB_SPIN_MAX) {
-        if (err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    NBS(cw += __builtin_amdgcn_s_memtime() - t0;)
-    asm volatile("" ::: "memory");
-  };
-  __builtin_amdgcn_s_setprio(3);
-  NBS(const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();)
-  wait_ready(0, 0u);
-  f32x4 cur[BQ], nxt[BQ];
-  {
-    const f32x4 *p0 = (const f32x4 *)&P[0][crow * LD];
-#pragma unroll
-    for (int j = 0; j < BQ; ++j) cur[j] = p0[j];
-  }
-  auto adds = [&]() { nb_add_batch<BQ>(acc, cur, nxt); };
-  for (int c = 0; c < nch; ++c) {
-    const f32x4 *pc = (const f32x4 *)&P[c % NB_RING][crow * LD];
-    const unsigned rdy = lds_load(&ready[cw_i][(c + 1) % NB_RING]);  // (as in chain32_nb_body)
-#pragma unroll
-    for (int q = 0; q < NBQ - 1; ++q) {
-#pragma unroll
-      for (int j = 0; j < BQ; ++j) nxt[j] = pc[(q + 1) * BQ + j];
-      adds();
-    }
-    __hip_atomic_store(&consw[cw_i], (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (c + 1 < nch && rdy < need(c + 1)) wait_ready(c + 1, rdy);
-    asm volatile("" ::: "memory");
-    const f32x4 *pn = (const f32x4 *)&P[(c + 1) % NB_RING][crow * LD];
-#pragma unroll
-    for (int j = 0; j < BQ; ++j) nxt[j] = pn[j];
-    adds();
-  }
-  NBS(if (lane == 0 && B.nj > 1 && cw_i == 0) {
-    g_nb_stamps[1024 + blockIdx.x][0] = c_t0;
-    g_nb_stamps[1024 + blockIdx.x][1] = __builtin_amdgcn_s_memtime();
-    g_nb_stamps[1024 + blockIdx.x][2] = cw;
-    g_nb_stamps[1024 + blockIdx.x][3] = nch;
-  })
-
-  // ----------------------------------------------------------------- epilogue
-  const int row = g * S::ROWS + crow;
-  const int rows = B.j[ji].w.rows;
-  const float *bias = B.j[ji].bias;
-  float *y = B.j[ji].y;
-  if (B.j[ji].epi == EPI_GELU_Q) {
-    const bool ok = row < rows;
-    float gv = 0.0f;
-    if (ok) {
-      gv = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
-      if (y) y[row] = gv;
-    }
-    const int blk = row / QK;
-    quantize_half(gv, lane, ok, B.j[ji].oq_qs + (size_t)blk * 16, B.j[ji].oq_d + blk,
-                  B.j[ji].oxd + (size_t)blk * QK);
-  } else if (row < rows) {
-    y[row] = bias ? acc + bias[row] : acc;
-  }
-  __builtin_amdgcn_s_setprio(0);
-}
-
-template <int CB, int PF, int CONS>
-__global__ void __launch_bounds__((64 * SoloShape<CB, CONS>::WAVES), 1) k_gemv_solo_nb(GemvBatch B, unsigned *err) {
-  __shared__ __attribute__((aligned(16))) float P[NB_RING][SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD];
-  __shared__ unsigned ready[CONS][NB_RING], consw[CONS];
-  solo_nb_body<CB, PF, CONS>(B, blockIdx.x, P, ready, consw, err);
-}
-
 template <int CB, int PF, int CONS>
 __global__ void __launch_bounds__((64 * SoloShape<CB, CONS>::WAVES), 1) k_gemv_solo(GemvBatch B) {
   __shared__ __attribute__((aligned(16))) float P[C5_RING][SoloShape<CB, CONS>::ROWS * SoloShape<CB, CONS>::LD];
@@ -1088,18 +906,7 @@ int launch_gemv_chain_batch(const GemvBatch &B, hipStream_t s) {
     tiles += B.j[i].w.tiles;
   }
   if (tiles == 0) return VSIM_OK;
-  static const int solo_nb = [] {
-    const char *e = getenv("VSIM_SOLO_NB");
-    return e ? atoi(e) : 0;
-  }();
-
-  if (gemv_chain_solo(B) && solo_nb == 1) {
-    hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)),
-                       dim3(64 * SoloShape<SOLO_CB, 1>::WAVES), 0, s, B, spin_error_counter());
-  } else if (gemv_chain_solo(B) && solo_nb == 2) {
-    hipLaunchKernelGGL((k_gemv_solo_nb<SOLO_CB, SOLO_PF, 2>), dim3(solo_groups(B, 2)),
-                       dim3(64 * SoloShape<SOLO_CB, 2>::WAVES), 0, s, B, spin_error_counter());
-  } else if (gemv_chain_solo(B)) {
+  if (gemv_chain_solo(B)) {
     hipLaunchKernelGGL((k_gemv_solo<SOLO_CB, SOLO_PF, 1>), dim3(solo_groups(B)), dim3(64 * SoloShape<SOLO_CB, 1>::WAVES),
                        0, s, B);
   } else {
