@@ -76,9 +76,13 @@ print("heads phases (us, medians): setup+RoPE %.2f  KQ %.2f  softmax %.2f  KQV %
 # the slowest fc_out tiles (end time, consumer wait per chunk, its producers' slot wait)
 fo = tl[:nf]
 order = np.argsort(-fo[:, 2])
-print("slowest fc_out tiles (index, XCD = index % 8, end us, consumer wait/chunk, producer slot wait/chunk, dma wait/chunk):")
-for i in order[:8]:
+print("slowest and median fc_out tiles (index, XCD = index % 8, end us, consumer wait/chunk, producer slot wait/chunk,"
+      " dma wait/chunk, consumer cycles, consumer us, GHz):")
+for i in list(order[:8]) + list(order[60:64]):
     b = buf[i]
     nchk = max(int(b[3]), 1)
-    print(f"  {i:4d} {i % 8} {us(fo[i, 2]):6.2f} {b[2] / nchk:7.0f} {np.median(b[12:20]) / nchk:7.0f} {np.median(b[4:12]) / nchk:7.0f}")
+    cyc = float(b[1] - b[0])
+    dur = (fo[i, 2] - fo[i, 0]) / 100.0
+    print(f"  {i:4d} {i % 8} {us(fo[i, 2]):6.2f} {b[2] / nchk:7.0f} {np.median(b[12:20]) / nchk:7.0f} {np.median(b[4:12]) / nchk:7.0f}"
+          f" {cyc:9.0f} {dur:6.2f} {cyc / dur / 1e3:5.2f}")
 print("end-time quartiles:", np.percentile(us(fo[:, 2]), [0, 25, 50, 75, 100]).round(2))

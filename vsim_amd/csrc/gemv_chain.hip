@@ -357,7 +357,11 @@ __device__ __forceinline__ unsigned lds_load(const unsigned *p) {
 }
 
 // SC1: the activation factors were written write-through by other workgroups of this launch
-template <class S, bool SC1>
+// ONE: B holds a single job (the tail's fc_out and out-projection): its arguments are read at
+// constant offsets with no job probe, so they load in one round trip at the workgroup's start
+// (the probe loop and the chosen job's fields behind it were three dependent kernarg round trips,
+// ~1.1 us from a tail workgroup's start to its first weight DMA, r05 stamps)
+template <class S, bool SC1, bool ONE = false>
 __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err) {
   constexpr int DEPTH = S::DEPTH, CB = S::CB, LD = S::LD, NPW = S::NPW;
   constexpr int WAIT_VM = waitcnt_vm(3 * (DEPTH - 1));  // chunk c landed, c+1 .. c+DEPTH-1 in flight
@@ -365,14 +369,19 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   int ji = 0;
-  while (ji < B.nj) {
-    if (t < B.j[ji].w.tiles) break;
-    t -= B.j[ji].w.tiles;
-    ++ji;
+  if constexpr (ONE) {
+    if (t >= B.j[0].w.tiles) return;
+  } else {
+    while (ji < B.nj) {
+      if (t < B.j[ji].w.tiles) break;
+      t -= B.j[ji].w.tiles;
+      ++ji;
+    }
+    if (ji >= B.nj) return;
+    ji = __builtin_amdgcn_readfirstlane(ji);
   }
-  if (ji >= B.nj) return;
-  ji = __builtin_amdgcn_readfirstlane(ji);
-  const int nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
+  const GemvJob &J = B.j[ONE ? 0 : ji];
+  const int nb = J.w.k / QK, nch = (nb + CB - 1) / CB;
   if (threadIdx.x < NB_RING) L.ready[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.cons = 0;
   __syncthreads();
@@ -383,9 +392,9 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
     const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
     if (p >= NPW) return;  // (a launch wider than this shape needs)
     const int o = 2 * p + hb;  // this lane's block within the chunk
-    const uint8_t *qs = B.j[ji].w.qs + (size_t)t * nb * T32 * 16 + (size_t)r * 16;
-    const float *dd = B.j[ji].w.d + (size_t)t * nb * T32 + r;
-    const float *xr = B.j[ji].xd + r;
+    const uint8_t *qs = J.w.qs + (size_t)t * nb * T32 * 16 + (size_t)r * 16;
+    const float *dd = J.w.d + (size_t)t * nb * T32 + r;
+    const float *xr = J.xd + r;
     // every chunk up to nch + DEPTH is loaded (block clamped), so the counted waits hold
     auto dma = [&](int c) {
       const int slot = c % DEPTH;
@@ -551,17 +560,17 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
 
   // ----------------------------------------------------------------- epilogue
   const int row = t * T32 + (lane & 31);
-  const int rows = B.j[ji].w.rows;
-  const float *bias = B.j[ji].bias;
-  float *y = B.j[ji].y;
-  if (B.j[ji].epi == EPI_GELU_Q) {
+  const int rows = J.w.rows;
+  const float *bias = J.bias;
+  float *y = J.y;
+  if (J.epi == EPI_GELU_Q) {
     const bool ok = lane < 32 && row < rows;
     float g = 0.0f;
     if (ok) {
-      g = h2f(B.j[ji].gelu_tab[f2h(acc + bias[row])]);
+      g = h2f(J.gelu_tab[f2h(acc + bias[row])]);
       if (y) y[row] = g;
     }
-    quantize_half(g, lane, ok, B.j[ji].oq_qs + (size_t)t * 16, B.j[ji].oq_d + t, B.j[ji].oxd + (size_t)t * QK);
+    quantize_half(g, lane, ok, J.oq_qs + (size_t)t * 16, J.oq_d + t, J.oxd + (size_t)t * QK);
   } else if (lane < 32 && row < rows) {
     y[row] = bias ? acc + bias[row] : acc;
   }
@@ -606,13 +615,16 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
     float a[sizeof(C2Lds<C2Tail>) / sizeof(float)];
   } L;
   int b = blockIdx.x;
+  // fc_out's producer arguments and the role bound in one kernel-argument round trip
+  asm volatile("" ::"s"(T.nf), "s"(T.f.j[0].w.qs), "s"(T.f.j[0].w.d), "s"(T.f.j[0].w.k), "s"(T.f.j[0].w.tiles),
+               "s"(T.f.j[0].xd));
   // (VSIM_NB_STAMPS: s_memrealtime timeline per workgroup in rows 1536.. : start, the role's
   // marks, end; tools/nb_stamps.py)
   NBS(unsigned long long *tl = g_nb_stamps[1536 + blockIdx.x];
       if (threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();)
   if (b < T.nf) {
     if constexpr (NBM & 1)
-      chain32_nb_body<C2Tail, false>(T.f, b, L.n, T.err);
+      chain32_nb_body<C2Tail, false, true>(T.f, b, L.n, T.err);
     else
       chain32_body(T.f, b, L.g);
     NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
@@ -643,7 +655,7 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   __syncthreads();
   NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
   if constexpr (NBM & 2)
-    chain32_nb_body<C2Tail, true>(T.o, b, L.n, T.err);
+    chain32_nb_body<C2Tail, true, true>(T.o, b, L.n, T.err);
   else
     chain32_body(T.o, b, L.g);
   NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
@@ -655,6 +667,10 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
       (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds<C2Tail>)) {
     set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
+    return VSIM_EINVAL;
+  }
+  if (f.nj > 1 || o.nj > 1) {
+    set_error("layer tail: fc_out and the out-projection are one job each");
     return VSIM_EINVAL;
   }
   TailJob T;
