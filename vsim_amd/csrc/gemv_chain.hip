@@ -13,9 +13,10 @@
 //    for the workgroup's rows into a 3-slot LDS ring, one s_barrier per chunk: in iteration
 //    k producers fill chunk k while the consumer adds chunk k-2 (and reads ahead into k-1).
 //
-// Two shapes: k_gemv_solo (64 rows per workgroup, the consumer alone on SIMD0, six producers
-// on SIMD1-3, for batches with many rows) and chain32_body (one 32-row tile per workgroup,
-// for fc_out / the out-projection, also the GEMV roles of k_layer_tail).
+// Shapes: k_gemv_solo (64 rows per workgroup, the consumer alone on SIMD0, six producers on
+// SIMD1-3, for batches with many rows), chain32_body (k_gemv_chain32: one 32-row tile per
+// workgroup, for batches with few rows) and chain32_nb_body (the GEMV roles of k_layer_tail:
+// 32-row tiles with a barrier-free hand-off and a pair-lane consumer, r05).
 // Epilogues: plain store (+bias), and fc_in's bias + GELU table + re-quantization of the
 // outputs into the next product's Q4_0 activation blocks (ggml.c:5024-5041).
 #include <cstdlib>
@@ -95,6 +96,9 @@ constexpr int C2_RING = 3, C2_WIN = 16;
 // us per tail, 601.2-604.6 tok/s at 248 tokens, against 12-block chunks 35.1 (591.8-592.8) and
 // the 8-block shape with wave 4 producing beside the consumer 36.0-36.3 (581.4-582.7); 3 chunks
 // ahead 34.8-34.9 (profiles/r04_tail_consumer_ab.txt)
+// r05, the barrier-free tail (chain32_nb_body only): rows padded to 8 banks for the pair-lane
+// consumer, four pair-term slots (NB_RING) and the LDS-DMA two chunks ahead, which is what the
+// LDS holds beside them (profiles/r05_tail_consumer_pairlane.txt)
 using C2Gemv = C2Shape<8, 4, false>;
 using C2Tail = C2Shape<16, 2, true, 8>;
 
@@ -580,25 +584,24 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
 // fc_out, the attention heads and the out-projection of one layer in one launch, so the
 // attention and the out-projection run beside fc_out, whose K = 4E chain is the layer's
 // longest dependency, instead of before it.  Roles by workgroup index:
-//   [0, nf)          fc_out tiles (32-row chain GEMV)
-//   [nf, nf + na)    attention heads (attn.hpp with this kernel's 5 waves); each head
-//                    stores the out-projection's operand write-through (sc1, CO = true),
-//                    drains them (vmcnt) and counts itself in *done (agent scope)
-//   [nf + na, ...)   out-projection tiles; wait until *done == na; their factor LDS-DMA is sc1
-//                    (device-coherent: it reads past stale lines in the XCD's L2), so neither
+//   [0, nf)          fc_out tiles (chain32_nb_body: 32 rows, 16-block chunks, eight producers,
+//                    the consumer alone on SIMD0)
+//   [nf, nf + na)    attention heads (attn.hpp; each head over nsplit workgroups, KQV columns
+//                    split); each stores the out-projection's operand write-through (sc1,
+//                    CO = true), drains it (vmcnt) and counts itself in *done (agent scope)
+//   [nf + na, ...)   out-projection tiles; wait until *done == na; their factor loads are sc1
+//                    (device-coherent: they read past stale lines in the XCD's L2), so neither
 //                    side needs a fence.  r04: the release fence (an L2 write-back per head)
 //                    and the acquire (an L2 invalidate, which also dropped fc_out's lines)
 //                    cost 38.9 vs 35.8-36.0 us per tail at the bench's 248 positions
 //                    (profiles/r04_tail_headpath_ab.txt)
 // Waiting workgroups only wait for lower-indexed ones, which the dispatcher places first on
 // this part (and fc_out's tiles never wait, so the CUs they hold always come free); the wait
-// is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it the error counter
-// (vsim_spin_timeouts) is bumped and the tile goes on.  r04 measured two placement-independent
-// role assignments (tools/tail_ab.sh): every role by a start-order ticket, 55.8 vs 40.9 us per
-// tail; heads pulled from a claim counter by the head workgroups and, when unclaimed, by the
-// out-projection tiles before they wait: a bloom-560m full-width decode differed from the
-// oracle at a late step (not understood; the variant without stealing passed).  Neither is
-// kept.  *done is zeroed by the layer's LayerNorm kernel.
+// is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it the per-device error counter
+// is bumped, the tile goes on, and the executor fails the call (VSIM_ESPIN).  *done is zeroed by
+// the layer's LayerNorm kernel.  r05 A/B of the barrier-free hand-off against r04's per-chunk
+// barrier (chain32_body): 31.4 vs 33.7 us per tail (profiles/r05_tail_nb_ab.txt); the barrier
+// tail is no longer built.
 constexpr unsigned TAIL_SPIN_MAX = 1u << 22;
 struct TailJob {
   GemvBatch f, o;
@@ -607,12 +610,10 @@ struct TailJob {
   int nf;
 };
 
-template <int NBM>
 __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   __shared__ union {
-    C2Lds<C2Tail> g;
     NbLds<C2Tail> n;
-    float a[sizeof(C2Lds<C2Tail>) / sizeof(float)];
+    float a[sizeof(NbLds<C2Tail>) / sizeof(float)];
   } L;
   int b = blockIdx.x;
   // fc_out's producer arguments and the role bound in one kernel-argument round trip
@@ -623,10 +624,7 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   NBS(unsigned long long *tl = g_nb_stamps[1536 + blockIdx.x];
       if (threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();)
   if (b < T.nf) {
-    if constexpr (NBM & 1)
-      chain32_nb_body<C2Tail, false, true>(T.f, b, L.n, T.err);
-    else
-      chain32_body(T.f, b, L.g);
+    chain32_nb_body<C2Tail, false, true>(T.f, b, L.n, T.err);
     NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
     return;
   }
@@ -654,10 +652,7 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   }
   __syncthreads();
   NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
-  if constexpr (NBM & 2)
-    chain32_nb_body<C2Tail, true, true>(T.o, b, L.n, T.err);
-  else
-    chain32_body(T.o, b, L.g);
+  chain32_nb_body<C2Tail, true, true>(T.o, b, L.n, T.err);
   NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
 }
 
@@ -665,7 +660,7 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
                       hipStream_t s) {
   const int S = a.nsplit > 1 ? a.nsplit : 1;
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
-      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(C2Lds<C2Tail>)) {
+      (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(NbLds<C2Tail>)) {
     set_error("layer tail: attention shape (head dim, n_ctx) outside the fused kernel's range");
     return VSIM_EINVAL;
   }
@@ -684,23 +679,11 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   int no = 0;
   for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;
   // one workgroup per CU (fc_out's consumer keeps its SIMD): the static LDS is above half the
-  // CU's already at DEPTH 8, the dynamic pad keeps it so at any depth; the workgroups that find
-  // no CU start as attention heads end
-  // the barrier-free hand-off (chain32_nb_body) for fc_out and the out-projection; r05 A/B
-  // against the per-chunk barrier (chain32_body): 31.4 vs 33.7 us per tail, 630-631 vs 605-607
-  // tok/s (profiles/r05_tail_nb_ab.txt).  VSIM_TAIL_NB = 0 (barrier), 1 (fc_out only), 2
-  // (out-projection only) rebuild the A/B.
-  static const int nbm = [] {
-    const char *e = getenv("VSIM_TAIL_NB");
-    return e ? atoi(e) & 3 : 3;
-  }();
+  // CU's (a dynamic pad would keep it so for a smaller shape); the workgroups that find no CU
+  // start as attention heads end
   const dim3 grid(T.nf + a.H * S + no), blk(C2Tail::THREADS);
-  constexpr size_t lds_static = sizeof(NbLds<C2Tail>) > sizeof(C2Lds<C2Tail>) ? sizeof(NbLds<C2Tail>) : sizeof(C2Lds<C2Tail>);
-  constexpr size_t pad = lds_static > 80 * 1024 ? 0 : 81 * 1024 - lds_static;  // (one workgroup per CU)
-  if (nbm == 0) hipLaunchKernelGGL(k_layer_tail<0>, grid, blk, pad, s, T);
-  if (nbm == 1) hipLaunchKernelGGL(k_layer_tail<1>, grid, blk, pad, s, T);
-  if (nbm == 2) hipLaunchKernelGGL(k_layer_tail<2>, grid, blk, pad, s, T);
-  if (nbm == 3) hipLaunchKernelGGL(k_layer_tail<3>, grid, blk, pad, s, T);
+  constexpr size_t pad = sizeof(NbLds<C2Tail>) > 80 * 1024 ? 0 : 81 * 1024 - sizeof(NbLds<C2Tail>);
+  hipLaunchKernelGGL(k_layer_tail, grid, blk, pad, s, T);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
