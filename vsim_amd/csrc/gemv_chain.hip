@@ -693,8 +693,14 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
 // consumer wave alone on SIMD0 (producers sharing its SIMD stretch each dependent add by a
 // VALU slot), CB producer waves on SIMD1-3, one Q4_0 block of the chunk for the 64 rows
 // each, so the activation factors are wave-uniform scalar loads and the LDS carries
-// nothing but pair terms.  Waves the hardware would place on SIMD0 (4, 8, ...) only join
-// the barriers.  Weights: register ring as k_gemv_chain2.
+// nothing but pair terms.  Waves the hardware places on the consumer's SIMD (4, 8, ...) only
+// join the barriers.  Weights: register ring as k_gemv_chain2.
+// Placement as measured (r05, tools/solo_placement.py, HW_ID stamps): waves w and w + 4 always
+// share a SIMD, but which SIMD wave 0 gets rotates per workgroup, and the two workgroups of a CU
+// always put their consumers on different SIMDs, each beside two of the other workgroup's
+// producers (SIMD loads 4 / 4 / 2 + consumer / 2 + consumer producers).  Roles re-assigned from
+// HW_ID so both consumers share one SIMD (4 / 4 / 4 producers) ran slower, 22.47 vs 21.96 us
+// (profiles/r05_solo_nb2_ab.txt).
 // CONS = 2: 128 rows per workgroup, two consumer waves (0 and 4: the waves of a workgroup go
 // to the SIMDs cyclically, so these two share one SIMD, where two independent chains
 // interleave without stretching each other) and 2 CB producers on the other three SIMDs
@@ -739,6 +745,9 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   g = __builtin_amdgcn_readfirstlane(g);
   const int tiles = B.j[ji].w.tiles, nb = B.j[ji].w.k / QK, nch = (nb + CB - 1) / CB;
   const int nit = (nch + 2 + PF) / (PF + 1) * (PF + 1);
+  // (VSIM_NB_STAMPS: where each wave runs, HW_ID | XCC_ID << 32, rows 512 + workgroup)
+  NBS(if (lane == 0 && gridDim.x < 512 && wave < 32) g_nb_stamps[512 + blockIdx.x][wave] =
+          (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) | (unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32;)
 
   if ((wave & 3) == 0 && (wave >> 2) >= CONS) {  // filler on the consumers' SIMD
     for (int k = 0; k < nit; ++k) __syncthreads();
