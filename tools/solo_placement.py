@@ -57,3 +57,7 @@ for a, b in two:
         s0 = simd[c, 0]
         shared += int(sum(1 for w in range(W) if w % 4 and simd[c, w] == s0) + sum(1 for w in range(W) if w % 4 and simd[o, w] == s0))
 print(f"  producer waves on a consumer's SIMD, summed over the two-group CUs' consumers: {shared}")
+# the consumer SIMDs of a two-group CU: (lower group's, higher group's)
+pairs = collections.Counter((int(simd[a, 0]), int(simd[b, 0])) for a, b in (sorted(v) for v in two))
+print(f"  consumer SIMD pairs (lower, higher group index): {dict(pairs)}")
+print(f"  group index gap of the two groups of a CU: {collections.Counter(b - a for a, b in (sorted(v) for v in two)).most_common(5)}")
