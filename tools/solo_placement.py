@@ -61,3 +61,14 @@ print(f"  producer waves on a consumer's SIMD, summed over the two-group CUs' co
 pairs = collections.Counter((int(simd[a, 0]), int(simd[b, 0])) for a, b in (sorted(v) for v in two))
 print(f"  consumer SIMD pairs (lower, higher group index): {dict(pairs)}")
 print(f"  group index gap of the two groups of a CU: {collections.Counter(b - a for a, b in (sorted(v) for v in two)).most_common(5)}")
+# the consumers' clocks over their loops (s_memtime cycles / s_memrealtime at 100 MHz)
+cl = buf[512:512 + G, 8:12].astype(np.int64)
+dm, dr = cl[:, 1] - cl[:, 0], cl[:, 3] - cl[:, 2]
+ghz = dm / (dr / 100.0) / 1e3
+print(f"  consumer loop: median {np.median(dr) / 100:.2f} us, shader clock median {np.median(ghz):.3f} GHz "
+      f"(p10 {np.percentile(ghz, 10):.3f}, p90 {np.percentile(ghz, 90):.3f})")
+t0 = cl[:, 2].min()
+st, en = (cl[:, 2] - t0) / 100.0, (cl[:, 3] - t0) / 100.0
+for name, sel in (("groups 0..255", slice(0, 256)), ("groups 256..447", slice(256, G))):
+    print(f"  {name}: consumer loop start med {np.median(st[sel]):.2f} max {st[sel].max():.2f} us, "
+          f"end med {np.median(en[sel]):.2f} max {en[sel].max():.2f} us")

@@ -832,6 +832,8 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   const int crow = 64 * wave / 4 + lane;  // this consumer's row within the group
   auto src = [&](int c) { return &P[c % C5_RING][crow * S::LD]; };
   __builtin_amdgcn_s_setprio(3);
+  // (VSIM_NB_STAMPS: the consumer's shader-clock and 100 MHz real-time stamps at its start and end)
+  NBS(const unsigned long long c_m0 = __builtin_amdgcn_s_memtime(), c_r0 = __builtin_amdgcn_s_memrealtime();)
   for (int k = 0; k < nit; ++k) {
     const int c = k - 2;
     if (c == -1 && nch > 0) {
@@ -861,6 +863,13 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
     }
     __syncthreads();
   }
+  NBS(if (lane == 0 && wave == 0 && gridDim.x < 512) {
+    unsigned long long *st = g_nb_stamps[512 + blockIdx.x];
+    st[8] = c_m0;
+    st[9] = __builtin_amdgcn_s_memtime();
+    st[10] = c_r0;
+    st[11] = __builtin_amdgcn_s_memrealtime();
+  })
 
   // ----------------------------------------------------------------- epilogue
   const int row = g * S::ROWS + crow;
