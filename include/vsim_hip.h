@@ -181,6 +181,11 @@ int vsim_norm_fallbacks(unsigned out[2]);
  * eval_argmax, generate, sync) return VSIM_ESPIN when their device's count grew. */
 int vsim_spin_timeouts(unsigned *out);
 int vsim_op_gelu(const float *x, float *y, int n, void *stream);
+/* Greedy token of a logit row: *out = numpy.argmax(x[0:n]) (first index among equal maxima, -0.0 ==
+ * +0.0, the first NaN if any); x and out device pointers.  The model's greedy step
+ * (vsim_model_eval_argmax / vsim_model_generate) runs the same kernel; replaces the reference's
+ * host-side greedy pick over the logits (cformers/interface.py, the sampling of vsim.cpp's main loop). */
+int vsim_op_argmax(const float *x, int n, int32_t *out, void *stream);
 /* scale -> diag_mask_inf(n_past) -> soft_max over p[nz][nr][nc], in place */
 int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream);
 /* style 0 = GPT-NeoX rotate-half (ggml.c:6086), 1 = GPT-J pairs (ggml.c:5919);

@@ -219,6 +219,45 @@ def test_norm_sequential_mean_sum_cases(n):
     assert hip.norm_fallbacks()[0] > before  # the fallback path ran
 
 
+def _argmax_rows(n, rng):
+    base = rng.standard_normal(n).astype(np.float32)
+    rows = {"random": base}
+    t = base.copy()  # the maximum at three indices: the first one wins
+    if n >= 3:
+        m = t.max() + 1
+        for i in sorted(rng.choice(n, 3, replace=False)):
+            t[i] = m
+    rows["ties"] = t
+    t = base.copy()
+    if n >= 2:
+        i, j = sorted(rng.choice(n, 2, replace=False))
+        t[j], t[i] = np.nan, np.nan  # the first NaN wins over every number
+    rows["nan"] = t
+    z = np.zeros(n, np.float32)
+    z[: (n + 1) // 2] = -0.0  # -0.0 equals +0.0: index 0
+    rows["zeros"] = z
+    rows["neg_inf"] = np.full(n, -np.inf, np.float32)
+    t = np.full(n, -np.inf, np.float32)
+    t[-1] = np.float32(-3.4e38)
+    rows["last"] = t
+    return rows
+
+
+@pytest.mark.parametrize("n", [1, 7, 1029, 50400, 250880, 262147])
+def test_argmax_numpy_conventions(n):
+    """vsim_op_argmax (the kernel of the model's greedy step) returns numpy.argmax: first of
+    equal maxima, -0.0 == +0.0, first NaN; rows from 1 value to BLOOM's vocabulary and past it,
+    on 16-byte-aligned and misaligned rows (the float4 path and the scalar path)."""
+    rng = np.random.default_rng(n)
+    out = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for name, row in _argmax_rows(n, rng).items():
+        for off in (0, 1):
+            buf = np.concatenate([np.zeros(off, np.float32), row])
+            xt = dev(buf)
+            hip.check(hip.lib().vsim_op_argmax(xt.data_ptr() + 4 * off, n, out.data_ptr(), None), "argmax")
+            assert int(out.item()) == int(np.argmax(row)), (name, off)
+
+
 def test_gelu_bit_exact():
     z = ops("gelu")
     x = dev(z["x"])

@@ -120,6 +120,15 @@ int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, cons
 int vsim_op_gelu(const float *x, float *y, int n, void *stream) {
   return launch_gelu(x, y, n, nullptr, 1, (hipStream_t)stream);
 }
+int vsim_op_argmax(const float *x, int n, int32_t *out, void *stream) {
+  unsigned long long *ws = nullptr;
+  VSIM_HIP(hipMalloc((void **)&ws, 2 * sizeof(unsigned long long)));
+  int rc = hipMemsetAsync(ws, 0, 2 * sizeof(unsigned long long), (hipStream_t)stream) == hipSuccess ? VSIM_OK : VSIM_EHIP;
+  if (rc == VSIM_OK) rc = launch_argmax(x, n, (int *)out, ws, (hipStream_t)stream);
+  if (rc == VSIM_OK && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = VSIM_EHIP;
+  (void)hipFree(ws);
+  return rc;
+}
 int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream) {
   return launch_attn_softmax(p, nc, nr, nz, n_past, scale, (hipStream_t)stream);
 }

@@ -275,7 +275,8 @@ int launch_norm(const float *x, float *y, int k, int rows, const float *w, const
 // prompt batches: the norm + affine of each row straight to the GEMM's fp16 operand
 // (launch_act_quant_f16 of launch_norm's output, in one kernel)
 int launch_norm_f16q(const float *x, void *x16, int k, int rows, const float *w, const float *b, hipStream_t s);
-int launch_argmax(const float *x, int n, int *out, hipStream_t s);
+// ws: 16 bytes of zeroed device memory per concurrent caller (the kernel leaves it zeroed)
+int launch_argmax(const float *x, int n, int *out, unsigned long long *ws, hipStream_t s);
 int launch_gemm_q4_f16(const W4 &W, const void *xq, int n, const float *bias, float *y, hipStream_t s);
 // fast-mode prompt batches (n >= GEMM_MIN_N): activation rows quantized (optionally after
 // bias + GELU) straight to the GEMM's fp16 operand x16 [n][K], and the GEMM on it
@@ -343,7 +344,8 @@ _Float16 *attn_prefill_vt16(void *scratch, int E, int nk);
 size_t attn_prefill_scratch(int E, int nk);
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
                       hipStream_t s);
-int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s);
+int launch_argmax_gen(const float *x, int n, int *out, unsigned long long *ws, int *tok, int *npast, int *hist,
+                      hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);
 int launch_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, hipStream_t s,
                         const float *alibi = nullptr);

@@ -90,6 +90,7 @@ struct vsim_model {
   hipGraphExec_t gexec_am = nullptr;
   int graph_am_mode = -1;
   int *am_dev = nullptr, *am_host = nullptr;
+  unsigned long long *am_ws = nullptr;  // the argmax's key and workgroup count (zero between launches)
   // device-resident greedy loop (vsim_model_generate): graph without uploads; the argmax
   // kernel feeds tok_dev / npast_dev and records into hist_dev[n_ctx]
   hipGraph_t graph_gen = nullptr;
@@ -162,6 +163,8 @@ void free_scratch(vsim_model *m) {
   if (m->gexec_am) (void)hipGraphExecDestroy(m->gexec_am);
   if (m->graph_am) (void)hipGraphDestroy(m->graph_am);
   if (m->am_dev) (void)hipFree(m->am_dev);
+  if (m->am_ws) (void)hipFree(m->am_ws);
+  m->am_ws = nullptr;
   if (m->am_host) (void)hipHostFree(m->am_host);
   m->gexec_am = nullptr;
   m->graph_am = nullptr;
@@ -247,6 +250,8 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMalloc((void **)&m->npast_dev, sizeof(int)));
   VSIM_HIP(hipHostMalloc((void **)&m->npast_host, sizeof(int), hipHostMallocDefault));
   VSIM_HIP(hipMalloc((void **)&m->am_dev, sizeof(int)));
+  VSIM_HIP(hipMalloc((void **)&m->am_ws, 2 * sizeof(unsigned long long)));
+  VSIM_HIP(hipMemset(m->am_ws, 0, 2 * sizeof(unsigned long long)));
   VSIM_HIP(hipHostMalloc((void **)&m->am_host, sizeof(int), hipHostMallocDefault));
   VSIM_HIP(hipMalloc((void **)&m->hist_dev, (size_t)m->n_ctx * sizeof(int)));
   // counters of the fused layer kernels at [0], [64], [128] (separate 256-byte lines)
@@ -1557,7 +1562,7 @@ int enqueue_stage(vsim_model *m, int &nk) {
   }
   RC(enqueue_decode(m, nk));
   if (m->last) {
-    RC(launch_argmax(m->logits, m->hp.n_vocab, m->st_tok_out, s));
+    RC(launch_argmax(m->logits, m->hp.n_vocab, m->st_tok_out, m->am_ws, s));
     ++nk;
   } else {
     VSIM_HIP(hipMemcpyAsync(m->st_resid_out, m->resid_final, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
@@ -1594,10 +1599,10 @@ int decode_graph(vsim_model *m, int kind) {
   }
   if (rc == 0 && stage) {
   } else if (rc == 0 && gen) {
-    rc = launch_argmax_gen(m->logits, V, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s);
+    rc = launch_argmax_gen(m->logits, V, m->am_dev, m->am_ws, m->tok_dev, m->npast_dev, m->hist_dev, s);
     ++gk;
   } else if (rc == 0 && argmax) {
-    rc = launch_argmax(m->logits, V, m->am_dev, s);
+    rc = launch_argmax(m->logits, V, m->am_dev, m->am_ws, s);
     ++gk;
     if (rc == 0 && hipMemcpyAsync(m->am_host, m->am_dev, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
       rc = hip_fail(hipErrorUnknown, "capture argmax copy");
@@ -1644,7 +1649,7 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
     int nk = 0;
     RC(upload_step(m));
     RC(enqueue_decode(m, nk));
-    RC(launch_argmax(m->logits, V, m->am_dev, s));
+    RC(launch_argmax(m->logits, V, m->am_dev, m->am_ws, s));
     VSIM_HIP(hipMemcpyAsync(m->am_host, m->am_dev, sizeof(int), hipMemcpyDeviceToHost, s));
     m->kernels_last = nk + 1;
   }
@@ -1681,7 +1686,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
       int nk = 0;
       m->prof_npast = n_past + i;
       RC(enqueue_decode(m, nk));
-      RC(launch_argmax_gen(m->logits, m->hp.n_vocab, m->am_dev, m->tok_dev, m->npast_dev, m->hist_dev, s));
+      RC(launch_argmax_gen(m->logits, m->hp.n_vocab, m->am_dev, m->am_ws, m->tok_dev, m->npast_dev, m->hist_dev, s));
       m->kernels_last = nk + 1;
     }
   }

@@ -264,91 +264,81 @@ int norm_stats(unsigned *out2) {
 
 // ------------------------------------------------------------------ greedy argmax
 // Index of the largest logit with numpy.argmax's conventions: the first index among equal
-// maxima, and the first NaN if there is one.  One 1024-thread workgroup.
-__device__ __forceinline__ bool am_better(float v, int i, float bv, int bi) {
-  const bool n = v != v, bn = bv != bv;
-  if (n != bn) return n;
-  if (n) return i < bi;
-  if (v != bv) return v > bv;
-  return i < bi;
+// maxima (-0.0 equal to +0.0), and the first NaN if there is one.  Each value and its index
+// become one 64-bit key whose unsigned order is that order: the value's bits mapped to an
+// unsigned order (NaN -> all ones, -0.0 -> +0.0) above ~index.  The workgroups reduce their
+// keys, fold them into ws[0] with one 64-bit atomic max each, then count themselves in ws[1];
+// the last to count reads the result and zeroes ws for the next launch.  r05: the single
+// 1024-thread workgroup this replaced pulled the whole 50k-logit row through one CU, 14.45 us
+// per token (profiles/r05_exact_kernel_stats.csv).
+__device__ __forceinline__ unsigned long long am_key(float v, int i) {
+  uint32_t u = __float_as_uint(v);
+  if (v != v) u = 0xFFFFFFFFu;
+  else if (v == 0.0f) u = 0x80000000u;
+  else u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (0xFFFFFFFFu - (uint32_t)i);
+}
+constexpr int AM_T = 256, AM_MAX_WG = 64;
+static int am_grid(const float *x, int n) {
+  const int n4 = ((uintptr_t)x & 15) ? 0 : n / 4;
+  const int per = n4 > n - 4 * n4 ? n4 : n - 4 * n4;  // float4 items or scalar items, whichever the grid walks more
+  const int g = (per + AM_T - 1) / AM_T;
+  return g < 1 ? 1 : g > AM_MAX_WG ? AM_MAX_WG : g;
 }
 // GEN: the device-resident greedy loop's epilogue -- the token also becomes the next step's
 // input (tok), is recorded at hist[n_past] and n_past advances (k_argmax is the last kernel
 // of the step, so every reader of n_past has run).
 template <bool GEN>
-__global__ void __launch_bounds__(1024) k_argmax(const float *__restrict__ x, int n, int *__restrict__ out,
-                                                 int *tok, int *npast, int *hist) {
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  float bv = -INFINITY;
-  int bi = 0x7FFFFFFF;
-  auto take = [&](float v, int i) {
-    if (am_better(v, i, bv, bi)) {
-      bv = v;
-      bi = i;
-    }
-  };
-  // float4 loads, AM_U per thread in flight (a loop of one dependent load per step was bound by
-  // the load latency: ~22 us for a 50k vocabulary); am_better is a total order, so the visiting
-  // order does not change the result
-  constexpr int AM_U = 16;
+__global__ void __launch_bounds__(AM_T) k_argmax(const float *__restrict__ x, int n, int *__restrict__ out,
+                                                 unsigned long long *ws, int *tok, int *npast, int *hist) {
+  __shared__ unsigned long long sk[AM_T / 64];
+  unsigned long long best = 0;
   const int n4 = ((uintptr_t)x & 15) ? 0 : n / 4;
+  const int gt = blockIdx.x * AM_T + threadIdx.x, nt = gridDim.x * AM_T;
   const float4 *x4 = (const float4 *)x;
-  for (int i0 = threadIdx.x; i0 < n4; i0 += 1024 * AM_U) {
-    float4 v[AM_U];
-#pragma unroll
-    for (int u = 0; u < AM_U; ++u) v[u] = x4[min(i0 + 1024 * u, n4 - 1)];
-#pragma unroll
-    for (int u = 0; u < AM_U; ++u) {
-      const int i = i0 + 1024 * u;
-      if (i < n4) {
-        take(v[u].x, 4 * i);
-        take(v[u].y, 4 * i + 1);
-        take(v[u].z, 4 * i + 2);
-        take(v[u].w, 4 * i + 3);
-      }
-    }
+  for (int i = gt; i < n4; i += nt) {
+    const float4 v = x4[i];
+    best = max(best, am_key(v.x, 4 * i));
+    best = max(best, am_key(v.y, 4 * i + 1));
+    best = max(best, am_key(v.z, 4 * i + 2));
+    best = max(best, am_key(v.w, 4 * i + 3));
   }
-  for (int i = 4 * n4 + threadIdx.x; i < n; i += 1024) take(x[i], i);
+  for (int i = 4 * n4 + gt; i < n; i += nt) best = max(best, am_key(x[i], i));
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float v = __shfl_xor(bv, o, 64);
-    const int i = __shfl_xor(bi, o, 64);
-    if (am_better(v, i, bv, bi)) {
-      bv = v;
-      bi = i;
-    }
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sv[w] = bv;
-    si[w] = bi;
-  }
+  for (int o = 32; o > 0; o >>= 1) best = max(best, (unsigned long long)__shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0) sk[threadIdx.x >> 6] = best;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < 16; ++k)
-      if (am_better(sv[k], si[k], bv, bi)) {
-        bv = sv[k];
-        bi = si[k];
-      }
-    *out = bi;
-    if (GEN) {
-      const int np = *npast;
-      *tok = bi;
-      hist[np] = bi;
-      *npast = np + 1;
-    }
+  if (threadIdx.x != 0) return;
+#pragma unroll
+  for (int w = 1; w < AM_T / 64; ++w) best = max(best, sk[w]);
+  unsigned *cnt = (unsigned *)(ws + 1);
+  __hip_atomic_fetch_max(ws, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the max is performed before this workgroup counts
+  if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x - 1) return;
+  const unsigned long long k = __hip_atomic_load(ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int bi = (int)(0xFFFFFFFFu - (uint32_t)k);
+  *out = bi;
+  if (GEN) {
+    const int np = *npast;
+    *tok = bi;
+    hist[np] = bi;
+    *npast = np + 1;
   }
+  __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-int launch_argmax(const float *x, int n, int *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_argmax<false>, dim3(1), dim3(1024), 0, s, x, n, out, nullptr, nullptr, nullptr);
+int launch_argmax(const float *x, int n, int *out, unsigned long long *ws, hipStream_t s) {
+  if (n <= 0) { set_error("argmax: empty row"); return VSIM_EINVAL; }
+  hipLaunchKernelGGL(k_argmax<false>, dim3(am_grid(x, n)), dim3(AM_T), 0, s, x, n, out, ws, nullptr, nullptr, nullptr);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }
 
-int launch_argmax_gen(const float *x, int n, int *out, int *tok, int *npast, int *hist, hipStream_t s) {
-  hipLaunchKernelGGL(k_argmax<true>, dim3(1), dim3(1024), 0, s, x, n, out, tok, npast, hist);
+int launch_argmax_gen(const float *x, int n, int *out, unsigned long long *ws, int *tok, int *npast, int *hist,
+                      hipStream_t s) {
+  if (n <= 0) { set_error("argmax: empty row"); return VSIM_EINVAL; }
+  hipLaunchKernelGGL(k_argmax<true>, dim3(am_grid(x, n)), dim3(AM_T), 0, s, x, n, out, ws, tok, npast, hist);
   VSIM_HIP(hipGetLastError());
   return VSIM_OK;
 }

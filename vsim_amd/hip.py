@@ -31,7 +31,7 @@ EXPORTS = [
     "vsim_op_q4_quantize", "vsim_op_q4_gemv", "vsim_op_q4_expand_f16", "vsim_op_gemm_f16",
     "vsim_op_act_quant_f16", "vsim_op_gemm_f16_gelu_q", "vsim_op_gemm_f16_rope", "vsim_op_gemm_f16_join",
     "vsim_op_gemm_q4_256", "vsim_op_get_rows",
-    "vsim_op_norm", "vsim_op_gelu", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv", "vsim_op_kq_causal", "vsim_op_kqv_causal",
+    "vsim_op_norm", "vsim_op_gelu", "vsim_op_argmax", "vsim_op_attn_softmax", "vsim_op_rope", "vsim_op_kq", "vsim_op_kqv", "vsim_op_kq_causal", "vsim_op_kqv_causal",
     "vsim_op_attn_prefill", "vsim_op_attn_prefill_q16", "vsim_gemm_set_streamk", "vsim_gemm_set_qk_pair", "vsim_gemm_set_tile_order", "vsim_op_gemm_q4_256_pair", "vsim_op_norm_f16q",
     "vsim_op_tables",
     "vsim_model_create", "vsim_model_load_file", "vsim_model_set_tensor", "vsim_model_get_tensor",
@@ -123,6 +123,7 @@ def lib():
     L.vsim_op_gemm_q4_256.argtypes = [vp, ci, ci, vp, ci, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp]
     L.vsim_op_norm.argtypes = [vp, vp, ci, ci, vp, vp, vp]
     L.vsim_op_gelu.argtypes = [vp, vp, ci, vp]
+    L.vsim_op_argmax.argtypes = [vp, ci, vp, vp]
     L.vsim_op_attn_softmax.argtypes = [vp, ci, ci, ci, ci, cf, vp]
     L.vsim_op_rope.argtypes = [ci, vp, ci, ci, ci, ci, ci, ci, vp]
     L.vsim_op_kq.argtypes = [vp, ci, vp, ci, ci, ci, ci, ci, vp, vp]
