@@ -175,16 +175,20 @@ int vsim_op_norm(const float *x, float *y, int k, int rows, const float *w, cons
 /* cumulative counts of exact-LayerNorm rows that needed the sequential fallback:
  * out[0] = mean not certified, out[1] = variance scale not certified (summed over devices) */
 int vsim_norm_fallbacks(unsigned out[2]);
-/* cumulative count of bounded cross-workgroup waits that gave up, summed over devices: the
- * fused layer tail's wait for its attention heads, the barrier-free chain GEMV's ring hand-off,
- * the prompt GEMM's stream-K finisher.  0 in every healthy run; the model calls (eval,
- * eval_argmax, generate, sync) return VSIM_ESPIN when their device's count grew. */
+/* cumulative count of bounded cross-workgroup waits that gave up, summed over devices and models:
+ * the fused layer tail's waits (its attention heads, the in-tail LayerNorm's granules), the
+ * barrier-free chain GEMV's ring hand-off, the prompt GEMM's stream-K finisher.  0 in every healthy
+ * run; the model calls (eval, eval_argmax, generate, sync) count their own launches' timeouts and
+ * return VSIM_ESPIN when that model's count grew. */
 int vsim_spin_timeouts(unsigned *out);
 int vsim_op_gelu(const float *x, float *y, int n, void *stream);
 /* Greedy token of a logit row: *out = numpy.argmax(x[0:n]) (first index among equal maxima, -0.0 ==
- * +0.0, the first NaN if any); x and out device pointers.  The model's greedy step
- * (vsim_model_eval_argmax / vsim_model_generate) runs the same kernel; replaces the reference's
- * host-side greedy pick over the logits (cformers/interface.py, the sampling of vsim.cpp's main loop). */
+ * +0.0, the first NaN if any); x and out device pointers; enqueued on stream, not synchronized.
+ * The model's greedy step (vsim_model_eval_argmax / vsim_model_generate) runs the same kernel in
+ * place of the reference's host-side greedy pick (sample_top_k with top_k = 1, utils.cpp:339-371,
+ * called from vsim.cpp's main loop).  Ties differ: the reference orders equal logits by
+ * std::partial_sort over (logit, id) pairs, whose order among equal keys the standard leaves
+ * unspecified; this kernel returns the first index, as numpy does.  Distinct maxima agree. */
 int vsim_op_argmax(const float *x, int n, int32_t *out, void *stream);
 /* scale -> diag_mask_inf(n_past) -> soft_max over p[nz][nr][nc], in place */
 int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream);

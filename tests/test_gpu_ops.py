@@ -247,7 +247,10 @@ def _argmax_rows(n, rng):
 def test_argmax_numpy_conventions(n):
     """vsim_op_argmax (the kernel of the model's greedy step) returns numpy.argmax: first of
     equal maxima, -0.0 == +0.0, first NaN; rows from 1 value to BLOOM's vocabulary and past it,
-    on 16-byte-aligned and misaligned rows (the float4 path and the scalar path)."""
+    on 16-byte-aligned and misaligned rows (the float4 path and the scalar path).  The tie rule
+    is numpy's, not the reference's: its greedy pick (sample_top_k, utils.cpp:339-371) orders
+    equal logits by std::partial_sort, which leaves their order unspecified; rows without ties
+    give the same index either way."""
     rng = np.random.default_rng(n)
     out = torch.zeros(1, dtype=torch.int32, device=DEV)
     for name, row in _argmax_rows(n, rng).items():

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <map>
 #include <vector>
 
 #include "common.hpp"
@@ -121,13 +122,23 @@ int vsim_op_gelu(const float *x, float *y, int n, void *stream) {
   return launch_gelu(x, y, n, nullptr, 1, (hipStream_t)stream);
 }
 int vsim_op_argmax(const float *x, int n, int32_t *out, void *stream) {
+  // one zeroed 16-byte workspace per (device, stream), kept: the kernel leaves it zeroed, so the
+  // call is a single launch (no allocation, no synchronization, capturable) like the model's
+  static std::mutex mu;
+  static std::map<std::pair<int, void *>, unsigned long long *> wss;
+  int dev = 0;
+  VSIM_HIP(hipGetDevice(&dev));
   unsigned long long *ws = nullptr;
-  VSIM_HIP(hipMalloc((void **)&ws, 2 * sizeof(unsigned long long)));
-  int rc = hipMemsetAsync(ws, 0, 2 * sizeof(unsigned long long), (hipStream_t)stream) == hipSuccess ? VSIM_OK : VSIM_EHIP;
-  if (rc == VSIM_OK) rc = launch_argmax(x, n, (int *)out, ws, (hipStream_t)stream);
-  if (rc == VSIM_OK && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = VSIM_EHIP;
-  (void)hipFree(ws);
-  return rc;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    unsigned long long *&w = wss[{dev, stream}];
+    if (!w) {
+      VSIM_HIP(hipMalloc((void **)&w, 2 * sizeof(unsigned long long)));
+      VSIM_HIP(hipMemset(w, 0, 2 * sizeof(unsigned long long)));
+    }
+    ws = w;
+  }
+  return launch_argmax(x, n, (int *)out, ws, (hipStream_t)stream);
 }
 int vsim_op_attn_softmax(float *p, int nc, int nr, int nz, int n_past, float scale, void *stream) {
   return launch_attn_softmax(p, nc, nr, nz, n_past, scale, (hipStream_t)stream);

@@ -91,8 +91,36 @@ struct LnQuantJob {
   // row = x + ((ja + jab) + (jf + jfb)), stored to jout when non-null
   const float *ja, *jab, *jf, *jfb;
   float *jout;
-  unsigned *clear;  // non-null: clear[0], [64], [128] zeroed by the kernel (fused-layer counters)
+  unsigned *clear;  // non-null: clear[256 * l] zeroed for l < nclear (the layer tails' head counters)
+  int nclear;
+  unsigned *ep;     // non-null: the decode step's epoch, advanced by one (the tail LayerNorm's tags)
 };
+
+// The next LayerNorm inside the layer tail (r06, k_layer_tail with TailJob::ln): the join
+// v = x + ((a + ab) + (f + fb)) of the layer's two branches (vsim.cpp:694-695), the norm
+// (ggml.c:4246-4304) from one round of per-tile partial sums, and the affine + Q4_0 quantize of
+// one 32-block per tile (ggml.c:5024-5041), for norm 1 and optionally norm 2 (GPT-NeoX parallel
+// residual: the post-attention norm of the same row).  Hand-offs inside the launch are data-
+// tagged granules (tag = epoch << 8 | layer + 1): out-projection tile t's outputs (og, 8-byte
+// {value, tag}), each tile's joined values (jg, for the fallback path) and partial sums (rec, two
+// 16-byte granules), all sc1 stores polled with sc1 loads.
+struct TailLn {
+  const float *x;            // residual in [E]
+  const float *ab, *fb;      // attention-output and MLP-output biases (ab may be null)
+  float *jout;               // joined residual out [E]
+  const float *w1, *b1;      // norm 1 affine
+  uint8_t *q1;               // norm 1 output, Q4 SoA: nibbles [E/32][16], then d
+  float *d1, *xd1;
+  const float *w2, *b2;      // norm 2 (null: one norm)
+  uint8_t *q2;
+  float *d2, *xd2;
+  unsigned long long *og, *jg;  // [E] granules
+  uint4 *rec;                // [2 * E/32] granules
+  const unsigned *ep;        // the step's epoch (written by the step's first k_ln_quant)
+  unsigned *stats;           // LayerNorm fallback counters (dev_stats)
+  int il;                    // layer index (tag)
+};
+constexpr int LNT_MAX_TILES = 256;  // E <= 8192
 
 struct AttnJob {
   const float *q, *k, *v;  // new rows [E] (Q, K, V after bias)
@@ -254,10 +282,13 @@ int tables_get(DevTables *t);  // lazily uploads host-built tables for the curre
 // Health counters of the current device (ops_elt.hip; null before tables_get on that device):
 // LayerNorm fallbacks, and the bounded cross-workgroup waits that gave up
 unsigned *dev_stats();
-unsigned *spin_error_counter();
+unsigned *spin_error_counter();  // the calling thread's target (set_spin_error_target) or the device's
+// the word the bounded waits of the launches this thread enqueues count into (null: the current
+// device's own counter); returns the previous target
+unsigned *set_spin_error_target(unsigned *p);
+void add_model_spin_timeouts(unsigned n);  // a model's timeouts, for vsim_spin_timeouts' total
 int norm_stats(unsigned *out2);              // LayerNorm fallbacks, summed over devices
 int spin_timeouts(unsigned *out);            // waits that gave up, summed over devices
-int spin_timeouts_dev(int dev, unsigned *out);
 
 int launch_q4_repack(const void *aos, void *soa, int rows, int k, hipStream_t s);
 int launch_q4_unpack(const void *soa, void *aos, int rows, int k, hipStream_t s);
@@ -342,8 +373,13 @@ int attn_prefill_ldt(int nk);  // V^T row length (keys padded to the key tile)
 _Float16 *attn_prefill_k16(void *scratch, int E, int nk);
 _Float16 *attn_prefill_vt16(void *scratch, int E, int nk);
 size_t attn_prefill_scratch(int E, int nk);
+// ln non-null (f and o one job each, both E rows): the tail also joins the residual and runs the
+// next LayerNorm(s) (TailLn); neither job's y is written (the joined row goes to ln->jout)
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
-                      hipStream_t s);
+                      hipStream_t s, const TailLn *ln = nullptr);
+// true when the tail LayerNorm can run for a model of width E on the current device (every
+// out-projection tile resident at once: E/32 tiles, one workgroup per CU)
+bool tail_ln_ok(int E);
 int launch_argmax_gen(const float *x, int n, int *out, unsigned long long *ws, int *tok, int *npast, int *hist,
                       hipStream_t s);
 int launch_gelu(const float *x, float *y, int n, const float *bias, int bias_len, hipStream_t s);

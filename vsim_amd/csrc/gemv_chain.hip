@@ -360,13 +360,239 @@ __device__ __forceinline__ unsigned lds_load(const unsigned *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ================================================================== the tail's LayerNorm (r06)
+// TailLn (common.hpp): the next layer's LayerNorm(s) computed inside the layer tail, so no
+// k_ln_quant launch (5.5 us) and no launch boundary sit between the tail and the next layer's
+// GEMV batch.  Per output tile t (32 rows):
+//  1. out-projection tile t stores its 32 sums as 8-byte granules {value, tag} (sc1), and is done;
+//  2. fc_out tile t (the tile's "owner": its K = 4E chain usually ends last, and it loads the
+//     out-projection's granules one chunk before its chain ends) joins the residual
+//     v = x + ((a + ab) + (f + fb)) (vsim.cpp:694-695, the order k_ln_quant's join keeps), stores
+//     v, and publishes the tile's partial sums as two 16-byte granules: sum v and min ulp (the
+//     exact-mean certificate's operands, ggml.c:4264-4270 summed in double), sum v^2 and an
+//     upper bound of sum |v|;
+//  3. every owner polls all tiles' partials (one round, no counter: the tags say which are in;
+//     r06: a drained store + agent counter polled by one lane, then one read of the partials,
+//     took the tail 36.5 vs 34.0 us, 639.4-639.8 vs 669.7-669.8 tok/s, profiles/r06_lnt_ab.txt),
+//     reduces them in one fixed order, so every owner derives the same mean and scale, then
+//     normalizes, applies the affine and quantizes its own 32-block (one Q4_0 block per tile).
+// fc_out tiles wait for higher-indexed workgroups here (the out-projection tiles): they hold at
+// most E/32 CUs, and the out-projection tiles wait for nothing but the heads, so they always get
+// the other CUs (tail_ln_ok: E/32 below the CU count).
+// The variance needs the mean, which a single round of partials cannot give exactly; it is
+// taken from the moments, s2 = (Q - 2 m S) + n m^2, and accepted when both ends of an error
+// interval covering this formula and the reference's sequential sum (ggml.c:4285-4293) give
+// the same float scale (the map S2 -> (float)(1/sqrt(S2/n + eps)) is monotone): the
+// certificate idea of ln_exact_lds_t with a wider interval.  Otherwise (an uncertified mean
+// or an ambiguous scale) the owners read the whole joined row back from its granules and run
+// ln_exact_lds_t's statistics on it: the sequential mean, the tree s2, the sequential s2.
+// Tags: epoch << 8 | layer + 1; the epoch is advanced by the step's first k_ln_quant, so a
+// granule left by an earlier step or layer never matches.
+constexpr unsigned LNT_SPIN_MAX = 1u << 22;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ unsigned lnt_tag(const TailLn &N) { return (*N.ep << 8) | (unsigned)(N.il + 1); }
+__device__ __forceinline__ void st_granule(unsigned long long *p, float v, unsigned tag) {
+  const unsigned long long g = (unsigned long long)__float_as_uint(v) | ((unsigned long long)tag << 32);
+  __hip_atomic_store((gu64 *)p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dwordx2 sc1
+}
+__device__ __forceinline__ unsigned long long ld_granule(const unsigned long long *p) {
+  return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dwordx2 sc1
+}
+__device__ __forceinline__ void st16_sc1(uint4 *p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ double dbl_of(unsigned lo, unsigned hi) {
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ void lnt_spin(unsigned &spins, unsigned *err, int lane) {
+  __builtin_amdgcn_s_sleep(1);
+  if (++spins == LNT_SPIN_MAX && err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// out-projection tile t, wave 0 (row t*32 + lane in lanes 0-31)
+__device__ __forceinline__ void lnt_oproj(const TailLn &N, int row, int rows, float acc, int lane) {
+  if (lane < 32 && row < rows) st_granule(N.og + row, acc, lnt_tag(N));
+  NBS(if (lane == 0) g_nb_stamps[1536 + blockIdx.x][8] = __builtin_amdgcn_s_memrealtime();)
+}
+
+// fc_out tile t, wave 0: acc = row t*32 + (lane & 31) of fc_out (lanes 32-63 hold copies); pre:
+// the out-projection's granule of that row as loaded a chunk before the chain ended; scr: LDS
+// for E floats (the fallback's copy of the joined row)
+__device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, float acc, unsigned long long pre,
+                                          float *scr, unsigned *err) {
+  const int lane = threadIdx.x & 63, i = t * T32 + (lane & 31), n = ntile * T32;
+  const unsigned tag = lnt_tag(N);
+  NBS(unsigned long long *ls = g_nb_stamps[1536 + blockIdx.x] + 8;
+      if (lane == 0) ls[0] = __builtin_amdgcn_s_memrealtime();)
+  // the join's and the affine's operands (earlier launches' data), loaded before any wait
+  const bool hi = lane >= 32, two = N.w2 != nullptr, mine = !hi || two;
+  const float xv = N.x[i], abv = N.ab ? N.ab[i] : 0.0f, fbv = N.fb ? N.fb[i] : 0.0f;
+  const float *wp = hi ? N.w2 : N.w1, *bp = hi ? N.b2 : N.b1;
+  const float wv = mine ? wp[i] : 0.0f, bv = mine ? bp[i] : 0.0f;
+  unsigned spins = 0;
+  // 1. the out-projection's value of row i
+  unsigned long long ga = pre;
+  while (!__all((unsigned)(ga >> 32) == tag) && spins < LNT_SPIN_MAX) {
+    lnt_spin(spins, err, lane);
+    ga = ld_granule(N.og + i);
+  }
+  NBS(if (lane == 0) ls[1] = __builtin_amdgcn_s_memrealtime();)
+  // 2. the join (ja + jab) + (jf + jfb), then x + that (kern.hpp ln_exact_lds_t's join)
+  const float a = N.ab ? __uint_as_float((unsigned)ga) + abv : __uint_as_float((unsigned)ga);
+  const float ff = N.fb ? acc + fbv : acc;
+  const float v = xv + (a + ff);
+  if (lane < 32) {
+    N.jout[i] = v;
+    st_granule(N.jg + i, v, tag);
+  }
+  {
+    double s = lane < 32 ? (double)v : 0.0, sa = lane < 32 ? (double)fabsf(v) : 0.0;
+    double q = lane < 32 ? (double)v * (double)v : 0.0;  // exact: 48-bit products
+    int um = lane < 32 ? ulp_exp(v) : (1 << 30);
+    s = wave_sum_d(s);
+    sa = wave_sum_d(sa);
+    q = wave_sum_d(q);
+    um = wave_min_i(um);
+    if (lane == 0) {
+      float au = (float)sa;  // rounded up: an upper bound of sum |v| is all the certificate needs
+      if ((double)au < sa) au = __uint_as_float(__float_as_uint(au) + 1u);
+      const unsigned long long sb = (unsigned long long)__double_as_longlong(s), qb = (unsigned long long)__double_as_longlong(q);
+      st16_sc1(N.rec + 2 * t, u32x4{(unsigned)sb, (unsigned)(sb >> 32), (unsigned)um, tag});
+      st16_sc1(N.rec + 2 * t + 1, u32x4{(unsigned)qb, (unsigned)(qb >> 32), __float_as_uint(au), tag});
+    }
+  }
+  NBS(if (lane == 0) ls[2] = __builtin_amdgcn_s_memrealtime();)
+  // 3. every tile's partials: granule g = lane + 64 k (even g: {sum, umin}, odd g: {sum v^2, sum |v|})
+  const int ng = 2 * ntile;
+  double S = 0.0, Q = 0.0, A = 0.0;
+  int U = 1 << 30;
+  spins = 0;
+  for (;;) {
+    u32x4 g[8];
+    const uint4 *p[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = N.rec + min(lane + 64 * k, ng - 1);
+    // (one statement: the loads and their wait, so no use of a result can move above the wait)
+    asm volatile(
+        "global_load_dwordx4 %0, %8, off sc1\n\t"
+        "global_load_dwordx4 %1, %9, off sc1\n\t"
+        "global_load_dwordx4 %2, %10, off sc1\n\t"
+        "global_load_dwordx4 %3, %11, off sc1\n\t"
+        "global_load_dwordx4 %4, %12, off sc1\n\t"
+        "global_load_dwordx4 %5, %13, off sc1\n\t"
+        "global_load_dwordx4 %6, %14, off sc1\n\t"
+        "global_load_dwordx4 %7, %15, off sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(g[0]), "=&v"(g[1]), "=&v"(g[2]), "=&v"(g[3]), "=&v"(g[4]), "=&v"(g[5]), "=&v"(g[6]), "=&v"(g[7])
+        : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+        : "memory");
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (lane + 64 * k < ng) ok = ok && g[k].w == tag;
+    if (__all(ok) || spins >= LNT_SPIN_MAX) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (lane + 64 * k >= ng) continue;
+        if ((lane & 1) == 0) {
+          S += dbl_of(g[k].x, g[k].y);
+          U = min(U, (int)g[k].z);
+        } else {
+          Q += dbl_of(g[k].x, g[k].y);
+          A += (double)__uint_as_float(g[k].z);
+        }
+      }
+      break;
+    }
+    lnt_spin(spins, err, lane);
+  }
+  NBS(if (lane == 0) ls[3] = __builtin_amdgcn_s_memrealtime();)
+  S = wave_sum_d(S);
+  Q = wave_sum_d(Q);
+  A = wave_sum_d(A);
+  U = wave_min_i(U);
+  const double eps = 1e-5f;
+  double mean = 0.0;
+  float scale = 0.0f;
+  const bool mean_ok = U == (1 << 30) || A * (1.0 + 0x1.0p-30) < ldexp(1.0, 53 + U);
+  bool fallback = !mean_ok;
+  if (mean_ok) {
+    // S is exact (every partial sum of the row is, under the certificate): the reference's mean
+    mean = S / n;
+    const double t1 = mean * S, t3 = (mean * mean) * n;
+    const double s2 = (Q - 2.0 * t1) + t3, M = Q + 2.0 * fabs(t1) + t3;
+    // |s2 - exact| <= ~20 u M (Q's tree, the three rounded terms); the reference's sequential
+    // s2 lies within (n + 5) u of the exact value (ggml.c:4287-4291): both inside B
+    const double B = ((2.0 * n + 64.0) * (s2 > 0.0 ? s2 : 0.0) + 64.0 * M) * 0x1.0p-53 * (1.0 + 0x1.0p-20);
+    const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
+    const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
+    if (sc_lo == sc_hi)
+      scale = sc_lo;
+    else
+      fallback = true;
+  }
+  if (fallback) {
+    // the whole joined row from its granules, then ln_exact_lds_t's statistics in one wave
+    for (int k = lane; k < n; k += 64) {
+      unsigned sp = 0;
+      unsigned long long g;
+      do {
+        g = ld_granule(N.jg + k);
+        if ((unsigned)(g >> 32) == tag) break;
+        __builtin_amdgcn_s_sleep(1);
+      } while (++sp < LNT_SPIN_MAX);
+      scr[k] = __uint_as_float((unsigned)g);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const double m = mean_ok ? S : seq_sum_exact_inl(scr, n, lane);
+    mean = m / n;
+    double s2 = 0.0;
+    for (int k = lane; k < n; k += 64) {
+      const double d = (double)scr[k] - mean;
+      s2 += d * d;
+    }
+    s2 = wave_sum_d(s2);
+    const double B = (2.0 * n + 64.0) * 0x1.0p-53 * s2;
+    const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
+    const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
+    scale = sc_lo;
+    if (sc_lo != sc_hi) {  // the reference's order, in lane 0
+      float sq = 0.0f;
+      if (lane == 0) {
+        double qq = 0.0;
+        for (int k = 0; k < n; ++k) {
+          const double d = (double)scr[k] - mean;
+          qq += d * d;
+        }
+        sq = (float)(1.0 / sqrt(qq / n + eps));
+      }
+      scale = __shfl(sq, 0);
+      if (t == 0 && lane == 0 && N.stats) atomicAdd(&N.stats[1], 1u);
+    }
+    if (!mean_ok && t == 0 && lane == 0 && N.stats) atomicAdd(&N.stats[0], 1u);
+  }
+  // 4. this tile's block: norm 1 in lanes 0-31, norm 2 in lanes 32-63 (same row values)
+  float y = (float)((double)v - mean);
+  y = y * scale;
+  const float z = mine ? (wv * y) + bv : 0.0f;
+  uint8_t *qs = hi ? N.q2 : N.q1;
+  float *dq = hi ? N.d2 : N.d1, *xd = hi ? N.xd2 : N.xd1;
+  quantize_half(z, lane, mine, mine ? qs + (size_t)t * 16 : nullptr, mine ? dq + t : nullptr,
+                mine ? xd + (size_t)t * QK : nullptr);
+  NBS(if (lane == 0) ls[4] = __builtin_amdgcn_s_memrealtime();)
+}
+
 // SC1: the activation factors were written write-through by other workgroups of this launch
 // ONE: B holds a single job (the tail's fc_out and out-projection): its arguments are read at
 // constant offsets with no job probe, so they load in one round trip at the workgroup's start
 // (the probe loop and the chosen job's fields behind it were three dependent kernarg round trips,
 // ~1.1 us from a tail workgroup's start to its first weight DMA, r05 stamps)
-template <class S, bool SC1, bool ONE = false>
-__device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err) {
+// LNR (the tail's LayerNorm, TailLn): 0 the job's own epilogue, 1 fc_out: the tile's owner, 2 the
+// out-projection's granules
+template <class S, bool SC1, bool ONE = false, int LNR = 0>
+__device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds<S> &L, unsigned *err,
+                                                const TailLn *N = nullptr) {
   constexpr int DEPTH = S::DEPTH, CB = S::CB, LD = S::LD, NPW = S::NPW;
   constexpr int WAIT_VM = waitcnt_vm(3 * (DEPTH - 1));  // chunk c landed, c+1 .. c+DEPTH-1 in flight
   static_assert(3 * (DEPTH - 1) < 64, "vmcnt immediate");
@@ -529,7 +755,12 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   rd(b0, 0, 0);
   rd(b1, 0, 1);
   rd(b2, 0, 2);
+  // (LNR 1: the out-projection's granule of this lane's row, loaded a chunk before the chain ends)
+  unsigned long long pre = 0;
+  const int c_pre = nch > 1 ? nch - 2 : 0;
   for (int c = 0; c < nch; ++c) {
+    if constexpr (LNR == 1)
+      if (c == c_pre) pre = ld_granule(N->og + t * T32 + (lane & 31));
     // the next chunk's count is read after batch NBQ-6's adds (behind the reads of batch NBQ-3,
     // so it lands with them) and compared at batch NBQ-3, before that chunk's first read; r05: read
     // at the chunk's top instead, it was often short by the chunk's last producers, and the
@@ -567,6 +798,14 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   const int rows = J.w.rows;
   const float *bias = J.bias;
   float *y = J.y;
+  if constexpr (LNR == 1) {
+    lnt_owner(*N, t, J.w.tiles, acc, pre, &L.P[0][0], err);
+    return;
+  }
+  if constexpr (LNR == 2) {
+    lnt_oproj(*N, row, rows, acc, lane);
+    return;
+  }
   if (J.epi == EPI_GELU_Q) {
     const bool ok = lane < 32 && row < rows;
     float g = 0.0f;
@@ -608,6 +847,8 @@ struct TailJob {
   AttnJob a;
   unsigned *done, *err;
   int nf;
+  int lnon;  // the next LayerNorm in this launch (TailLn)
+  TailLn ln;
 };
 
 __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
@@ -624,7 +865,10 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   NBS(unsigned long long *tl = g_nb_stamps[1536 + blockIdx.x];
       if (threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();)
   if (b < T.nf) {
-    chain32_nb_body<C2Tail, false, true>(T.f, b, L.n, T.err);
+    if (T.lnon)
+      chain32_nb_body<C2Tail, false, true, 1>(T.f, b, L.n, T.err, &T.ln);
+    else
+      chain32_nb_body<C2Tail, false, true>(T.f, b, L.n, T.err);
     NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
     return;
   }
@@ -652,12 +896,24 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   }
   __syncthreads();
   NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
-  chain32_nb_body<C2Tail, true, true>(T.o, b, L.n, T.err);
+  if (T.lnon)
+    chain32_nb_body<C2Tail, true, true, 2>(T.o, b, L.n, T.err, &T.ln);
+  else
+    chain32_nb_body<C2Tail, true, true>(T.o, b, L.n, T.err);
   NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
 }
 
+bool tail_ln_ok(int E) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  // every owner waits for every other owner's partials: all E/32 out-projection tiles must be
+  // resident at once (one workgroup per CU), beside at least one CU for the rest
+  return E % T32 == 0 && E / T32 <= LNT_MAX_TILES && E / T32 < cus;
+}
+
 int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
-                      hipStream_t s) {
+                      hipStream_t s, const TailLn *ln) {
   const int S = a.nsplit > 1 ? a.nsplit : 1;
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
       (size_t)attn_lds_floats(a.d, n_ctx) * sizeof(float) > sizeof(NbLds<C2Tail>)) {
@@ -668,13 +924,24 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
     set_error("layer tail: fc_out and the out-projection are one job each");
     return VSIM_EINVAL;
   }
-  TailJob T;
+  TailJob T{};
   T.f = f;
   T.o = o;
   T.a = a;
   T.done = done;
   T.err = spin_error_counter();
   T.nf = 0;
+  if (ln) {
+    const int E = o.nj == 1 ? o.j[0].w.rows : 0;
+    if (f.nj != 1 || o.nj != 1 || f.j[0].w.rows != E || a.d * a.H != E || !tail_ln_ok(E) || ln->il < 0 ||
+        ln->il > 254 || !ln->x || !ln->jout || !ln->w1 || !ln->b1 || !ln->q1 || !ln->d1 || !ln->xd1 || !ln->og ||
+        !ln->jg || !ln->rec || !ln->ep || (ln->w2 && (!ln->b2 || !ln->q2 || !ln->d2 || !ln->xd2))) {
+      set_error("layer tail: the in-tail LayerNorm needs fc_out and the out-projection over E rows, E/32 below the CU count");
+      return VSIM_EINVAL;
+    }
+    T.lnon = 1;
+    T.ln = *ln;
+  }
   for (int i = 0; i < f.nj; ++i) T.nf += f.j[i].w.tiles;
   int no = 0;
   for (int i = 0; i < o.nj; ++i) no += o.j[i].w.tiles;

@@ -223,7 +223,7 @@ __device__ __forceinline__ double rl_d(double v, int l) {  // lane l's v (l wave
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-__device__ __noinline__ double seq_sum_exact(const float *row, int n, int lane) {
+__device__ __forceinline__ double seq_sum_exact_inl(const float *row, int n, int lane) {
   constexpr int CAP = 32;
   const int n4 = n / 4;
   double s = 0.0;
@@ -291,6 +291,7 @@ __device__ __noinline__ double seq_sum_exact(const float *row, int n, int lane) 
   }
   return s;
 }
+__device__ __noinline__ double seq_sum_exact(const float *row, int n, int lane) { return seq_sum_exact_inl(row, n, lane); }
 
 // ------------------------------------------------------------------ exact LayerNorm core
 // ggml_compute_forward_norm_f32 (ggml.c:4246-4304) for one row by one NT-thread block,

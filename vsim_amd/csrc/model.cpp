@@ -46,7 +46,8 @@ struct LayerW {
 
 struct vsim_model {
   int arch = VSIM_ARCH_GPTNEOX;
-  unsigned spin_seen = 0;  // the device's spin-timeout count at the last check (spin_check)
+  unsigned *err_dev = nullptr, *err_host = nullptr;  // this model's bounded-wait timeouts (spin_check)
+  unsigned err_seen = 0;
   vsim_hparams hp{};
   int n_ctx = 512, device = 0, l0 = 0, l1 = 0;
   bool first = true, last = true;
@@ -109,7 +110,12 @@ struct vsim_model {
   hipGraphExec_t gexec_st = nullptr;
   int graph_st_mode = -1;
   int st_npast = -1;
-  unsigned *tail_done = nullptr;  // attention heads finished in the fused layer tail
+  unsigned *tail_done = nullptr;  // attention heads finished in the fused layer tail, one set per layer
+  // the tail LayerNorm's hand-off buffers (TailLn): the step epoch, the out-projection's and the joined row's
+  // granules [E], the per-tile partial sums [2 E/32]; zeroed at allocation (tag 0 never matches)
+  unsigned *lnt_ep = nullptr;
+  unsigned long long *lnt_og = nullptr, *lnt_jg = nullptr;
+  uint4 *lnt_rec = nullptr;
   // fast-mode decode step (fast_decode.hip): fc_out split-K partial rows and attention
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
   float *fast_ffp = nullptr, *fast_part = nullptr;
@@ -175,6 +181,10 @@ void free_scratch(vsim_model *m) {
   if (m->hist_dev) (void)hipFree(m->hist_dev);
   if (m->tail_done) (void)hipFree(m->tail_done);
   m->tail_done = nullptr;
+  if (m->lnt_ep) (void)hipFree(m->lnt_ep);
+  m->lnt_ep = nullptr;
+  m->lnt_og = m->lnt_jg = nullptr;
+  m->lnt_rec = nullptr;
   if (m->pf_scratch) (void)hipFree(m->pf_scratch);
   m->pf_scratch = nullptr;
   if (m->pf_x16) (void)hipFree(m->pf_x16);
@@ -259,6 +269,17 @@ int ensure_scratch(vsim_model *m, int N) {
   const size_t ncnt = (size_t)std::max(1, m->l1 - m->l0) * 256;
   VSIM_HIP(hipMalloc((void **)&m->tail_done, ncnt * sizeof(unsigned)));
   VSIM_HIP(hipMemset(m->tail_done, 0, ncnt * sizeof(unsigned)));
+  {
+    // one allocation: epoch (own 256-byte line), og [E], jg [E], rec [2 E/32]
+    const size_t lb = 256 + 2 * E * sizeof(unsigned long long) + 2 * (E / QK) * sizeof(uint4);
+    uint8_t *p = nullptr;
+    VSIM_HIP(hipMalloc((void **)&p, lb));
+    VSIM_HIP(hipMemset(p, 0, lb));
+    m->lnt_ep = (unsigned *)p;
+    m->lnt_og = (unsigned long long *)(p + 256);
+    m->lnt_jg = m->lnt_og + E;
+    m->lnt_rec = (uint4 *)(m->lnt_jg + E);
+  }
   {
     const size_t d = E / H, nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
     VSIM_HIP(fa(&m->fast_ffp, 8 * E));
@@ -448,16 +469,30 @@ void bind_pointers(vsim_model *m) {
     if (rc_) return rc_;         \
   } while (0)
 
-// After a call's work has been synchronized: a bounded cross-workgroup wait on this device that
-// gave up since the last check (k_layer_tail, the barrier-free chain GEMV, the stream-K
-// finisher) means some tile went on with incomplete data, so the call fails with VSIM_ESPIN
-// instead of returning results that are not the reference's.
+// Bounded cross-workgroup waits that gave up (k_layer_tail, the barrier-free chain GEMV, the
+// stream-K finisher) count into the model's own device word (m->err_dev: every launch this model
+// enqueues gets it through ErrScope, so another model's or a standalone op's timeout never fails
+// this one).  spin_read enqueues its copy to pinned host memory ahead of the call's stream sync;
+// spin_check, after that sync, fails the call with VSIM_ESPIN when it grew: some tile went on
+// with incomplete data, so the results are not the reference's.
+struct ErrScope {
+  unsigned *old;
+  explicit ErrScope(vsim_model *m) : old(set_spin_error_target(m->err_dev)) {}
+  ~ErrScope() { set_spin_error_target(old); }
+};
+int spin_read(vsim_model *m) {
+  VSIM_HIP(hipMemcpyAsync(m->err_host, m->err_dev, sizeof(unsigned), hipMemcpyDeviceToHost, m->stream));
+  return VSIM_OK;
+}
 int spin_check(vsim_model *m) {
-  unsigned n = 0;
-  RC(spin_timeouts_dev(m->device, &n));
-  if (n > m->spin_seen) {
-    const unsigned grew = n - m->spin_seen;
-    m->spin_seen = n;
+  const unsigned n = *(volatile unsigned *)m->err_host;
+  if (n > m->err_seen) {
+    const unsigned grew = n - m->err_seen;
+    m->err_seen = n;
+    add_model_spin_timeouts(grew);
+    // a workgroup that gave up may have left the argmax workspace mid-update: zero it again
+    (void)hipMemsetAsync(m->am_ws, 0, 2 * sizeof(unsigned long long), m->stream);
+    (void)hipStreamSynchronize(m->stream);
     set_error("a bounded cross-workgroup wait gave up " + std::to_string(grew) +
               " time(s) in this call (device " + std::to_string(m->device) + "): results not valid");
     return VSIM_ESPIN;
@@ -918,7 +953,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
   // residual buffers, so both norm workgroups of GPT-NeoX can read the old one.
   float *R[2] = {m->inpL, m->inpL2};
   int cur = 0;
-  bool pending = false;
+  bool pending = false, ln_done = false;
   const float *pend_a = nullptr, *pend_ab = nullptr, *pend_fb = nullptr;
   auto join_into = [&](LnQuantJob &j, bool write) {
     j.ja = pend_a;
@@ -940,6 +975,9 @@ int enqueue_decode(vsim_model *m, int &nk) {
   };
   // the attention heads fuse into k_layer_tail while their LDS (scores over n_ctx) fits it
   const bool tail = m->mode == VSIM_MODE_EXACT && (size_t)attn_lds_floats(d, m->n_ctx) * sizeof(float) <= 75264;
+  // the next layer's LayerNorm inside the tail (TailLn; parallel-residual graphs: the tail is
+  // where both branches of the layer end)
+  const bool lnt_ok = tail && !serial && m->l1 <= 255 && tail_ln_ok(E);
   auto attn_job = [&](size_t loff) {
     AttnJob A{};
     A.q = m->Qb;
@@ -955,16 +993,15 @@ int enqueue_decode(vsim_model *m, int &nk) {
     A.n_rot = bloom ? 0 : m->hp.n_rot;
     A.style = gptj ? 1 : 0;
     A.n_ctx = m->n_ctx;
-    // each head over two workgroups (its KQV columns halved; the scores computed by both): r05,
-    // 248-token lines 608.9 / 612.5 vs 606.9 / 610.8 tok/s unsplit, 602.6 / 601.3 at four
-    // (profiles/r05_tail_variants_ab.txt).  The largest split <= VSIM_ATT_SPLIT (default 2)
-    // whose column parts are whole 32-blocks.
-    static const int att_split = [] {
-      const char *e = getenv("VSIM_ATT_SPLIT");
-      return e ? atoi(e) : 2;
-    }();
+    // each head over two workgroups (its KQV columns halved; the scores computed by both) in the
+    // parallel-residual fused tail, where it was measured: r05, 248-token GPT-J lines 608.9 / 612.5
+    // vs 606.9 / 610.8 tok/s unsplit, 602.6 / 601.3 at four (profiles/r05_tail_variants_ab.txt).
+    // The largest split <= ATT_SPLIT whose column parts are whole 32-blocks; the serial graphs'
+    // heads and the standalone k_attn_decode stay one workgroup per head.  (A/B builds:
+    // tools/build_variant.sh NAME model.cpp 's/ATT_SPLIT = 2/ATT_SPLIT = 1/'.)
+    constexpr int ATT_SPLIT = 2;
     A.nsplit = 1;
-    for (int sp = att_split; sp > 1; --sp)
+    for (int sp = tail && !serial ? ATT_SPLIT : 1; sp > 1; --sp)
       if (d % sp == 0 && (d / sp) % QK == 0) {
         A.nsplit = sp;
         break;
@@ -995,7 +1032,10 @@ int enqueue_decode(vsim_model *m, int &nk) {
       // 1. (join +) input LayerNorm + quantize
       LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
       if (pending) join_into(j1, true);
-      if (tail) j1.clear = m->tail_done;
+      if (tail) {
+        j1.clear = m->tail_done;
+        j1.nclear = 1;
+      }
       long ev = prof_begin(m);
       RC(launch_ln_quant(j1, nullptr, E, s));
       prof_end(m, ev, "k_ln_quant", ln_bytes(1, pending));
@@ -1056,19 +1096,31 @@ int enqueue_decode(vsim_model *m, int &nk) {
       pend_fb = L.bproj;
       continue;
     }
-    // 1. (join +) LayerNorm(s) + quantize
-    LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
-    LnQuantJob j2{R[cur], L.ln2_w, L.ln2_b, q2, d2, m->xd2};
-    if (pending) {
-      join_into(j1, true);
-      join_into(j2, false);
+    // 1. (join +) LayerNorm(s) + quantize, unless the previous layer's tail ran them (TailLn)
+    unsigned *done = m->tail_done + 256 * (il - m->l0);  // this layer's head counter
+    long ev = -1;
+    if (!ln_done) {
+      LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
+      LnQuantJob j2{R[cur], L.ln2_w, L.ln2_b, q2, d2, m->xd2};
+      if (pending) {
+        join_into(j1, true);
+        join_into(j2, false);
+      }
+      if (tail && il == m->l0) {  // the step's first norm: every layer's counter, the epoch
+        j1.clear = m->tail_done;
+        j1.nclear = m->l1 - m->l0;
+        j1.ep = m->lnt_ep;
+      } else if (tail) {
+        j1.clear = done;
+        j1.nclear = 1;
+      }
+      ev = prof_begin(m);
+      RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
+      prof_end(m, ev, "k_ln_quant", ln_bytes(gptj ? 1 : 2, pending));
+      ++nk;
+      if (pending) cur ^= 1;
     }
-    if (tail) j1.clear = m->tail_done;
-    long ev = prof_begin(m);
-    RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
-    prof_end(m, ev, "k_ln_quant", ln_bytes(gptj ? 1 : 2, pending));
-    ++nk;
-    if (pending) cur ^= 1;
+    ln_done = false;
     // 2. {fc_in (+bias, GELU, requantize), Q, K, V}
     GemvBatch B{};
     B.nj = 4;
@@ -1093,9 +1145,51 @@ int enqueue_decode(vsim_model *m, int &nk) {
     job(Bf, 0, L.wproj, E, F, m->xd3, q3, d3, nullptr, m->ff);
     Bo.nj = 1;
     job(Bo, 0, L.wo, E, E, m->xda, qa, da, nullptr, m->attn);
+    // the next LayerNorm inside this tail: every layer but a non-last stage's last one
+    const bool lnt = tail && lnt_ok && (il + 1 < m->l1 || m->last);
+    if (lnt) {
+      TailLn N{};
+      N.x = R[cur];
+      N.ab = gptj ? nullptr : L.bo;
+      N.fb = L.bproj;
+      N.jout = R[cur ^ 1];
+      if (il + 1 < m->l1) {  // the next layer's input norm(s)
+        const LayerW &Ln = m->layers[il + 1 - m->l0];
+        N.w1 = Ln.ln1_w;
+        N.b1 = Ln.ln1_b;
+        if (!gptj) {
+          N.w2 = Ln.ln2_w;
+          N.b2 = Ln.ln2_b;
+          N.q2 = q2;
+          N.d2 = d2;
+          N.xd2 = m->xd2;
+        }
+      } else {  // the final norm, for the lm_head
+        N.w1 = m->lnf_w;
+        N.b1 = m->lnf_b;
+      }
+      N.q1 = q1;
+      N.d1 = d1;
+      N.xd1 = m->xd1;
+      N.og = m->lnt_og;
+      N.jg = m->lnt_jg;
+      N.rec = m->lnt_rec;
+      N.ep = m->lnt_ep;
+      N.stats = dev_stats();
+      N.il = il;
+      ev = prof_begin(m);
+      RC(launch_layer_tail(Bf, Bo, A, done, m->n_ctx, s, &N));
+      prof_end(m, ev, "k_layer_tail (fc_out + attention + out-proj + join + LayerNorm)",
+               w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + kv_bytes + ln_bytes(N.w2 ? 2 : 1, true));
+      ++nk;
+      cur ^= 1;
+      ln_done = true;
+      pending = false;
+      continue;
+    }
     if (tail) {
       ev = prof_begin(m);
-      RC(launch_layer_tail(Bf, Bo, A, m->tail_done, m->n_ctx, s));
+      RC(launch_layer_tail(Bf, Bo, A, done, m->n_ctx, s));
       prof_end(m, ev, "k_layer_tail (fc_out + attention + out-proj)",
                w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + kv_bytes);
       ++nk;
@@ -1118,17 +1212,19 @@ int enqueue_decode(vsim_model *m, int &nk) {
     pend_fb = L.bproj;
   }
   if (m->last) {
-    LnQuantJob jf{R[cur], m->lnf_w, m->lnf_b, q1, d1, m->xd1};
-    if (pending) join_into(jf, true);
-    long ev = prof_begin(m);
-    RC(launch_ln_quant(jf, nullptr, E, s));
-    prof_end(m, ev, "k_ln_quant", ln_bytes(1, pending));
-    ++nk;
-    if (pending) cur ^= 1;
+    if (!ln_done) {
+      LnQuantJob jf{R[cur], m->lnf_w, m->lnf_b, q1, d1, m->xd1};
+      if (pending) join_into(jf, true);
+      long ev = prof_begin(m);
+      RC(launch_ln_quant(jf, nullptr, E, s));
+      prof_end(m, ev, "k_ln_quant", ln_bytes(1, pending));
+      ++nk;
+      if (pending) cur ^= 1;
+    }
     GemvBatch B{};
     B.nj = 1;
     job(B, 0, m->lmh, V, E, m->xd1, q1, d1, gptj ? m->lmh_b : nullptr, m->logits);
-    ev = prof_begin(m);
+    const long ev = prof_begin(m);
     RC(launch_gemv_epi(B, m->mode, s));
     prof_end(m, ev, m->mode == VSIM_MODE_EXACT ? "k_gemv_solo (lm_head)" : "k_gemv_fast_epi (lm_head)",
              w4_algo_bytes(B.j[0].w));
@@ -1269,7 +1365,10 @@ int model_create_impl(int arch, const vsim_hparams *hp, int n_ctx, int device, i
   }
   DevTables t;
   if (int rc = tables_get(&t)) return fail(rc);
-  if (int rc = spin_timeouts_dev(m->device, &m->spin_seen)) return fail(rc);  // earlier calls' count
+  if (hipMalloc((void **)&m->err_dev, sizeof(unsigned)) != hipSuccess || hipMemset(m->err_dev, 0, sizeof(unsigned)) != hipSuccess ||
+      hipHostMalloc((void **)&m->err_host, sizeof(unsigned), hipHostMallocDefault) != hipSuccess)
+    return fail(VSIM_ENOMEM);
+  *m->err_host = 0;
   if (int rc = ensure_scratch(m, 16)) return fail(rc);
   *out = m;
   return VSIM_OK;
@@ -1305,6 +1404,8 @@ void vsim_model_free(vsim_model *m) {
   if (m->kcache && !m->borrowed) (void)hipFree(m->kcache);
   if (m->vcache && !m->borrowed) (void)hipFree(m->vcache);
   if (m->rope_cs) (void)hipFree(m->rope_cs);
+  if (m->err_dev) (void)hipFree(m->err_dev);
+  if (m->err_host) (void)hipHostFree(m->err_host);
   if (m->stream) (void)gemm_release_stream(m->stream);  // the prompt GEMM's stream-K workspace
   if (m->stream) (void)hipStreamDestroy(m->stream);
   for (hipEvent_t e : m->prof_events) (void)hipEventDestroy(e);
@@ -1633,6 +1734,7 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
   }
   if (n_past < 0 || n_past + 1 > m->n_ctx) { set_error("eval_argmax: n_past + 1 exceeds n_ctx"); return VSIM_EINVAL; }
   VSIM_HIP(hipSetDevice(m->device));
+  const ErrScope es(m);
   RC(ensure_scratch(m, 1));
   const int V = m->hp.n_vocab;
   if (token < 0 || token >= V) { set_error("eval_argmax: token id out of range"); return VSIM_EINVAL; }
@@ -1653,6 +1755,7 @@ int vsim_model_eval_argmax(vsim_model *m, int n_past, int32_t token, int32_t *ne
     VSIM_HIP(hipMemcpyAsync(m->am_host, m->am_dev, sizeof(int), hipMemcpyDeviceToHost, s));
     m->kernels_last = nk + 1;
   }
+  RC(spin_read(m));
   VSIM_HIP(hipStreamSynchronize(s));
   RC(spin_check(m));
   *next_token = m->am_host[0];
@@ -1669,6 +1772,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
   if (n_past < 0 || n_past + n_steps > m->n_ctx) { set_error("generate: n_past + n_steps exceeds n_ctx"); return VSIM_EINVAL; }
   if (n_steps == 0) return VSIM_OK;
   VSIM_HIP(hipSetDevice(m->device));
+  const ErrScope es(m);
   RC(ensure_scratch(m, 1));
   if (token < 0 || token >= m->hp.n_vocab) { set_error("generate: token id out of range"); return VSIM_EINVAL; }
   hipStream_t s = m->stream;
@@ -1691,6 +1795,7 @@ int vsim_model_generate(vsim_model *m, int n_past, int32_t token, int n_steps, i
     }
   }
   VSIM_HIP(hipMemcpyAsync(tokens_out, m->hist_dev + n_past, sizeof(int32_t) * n_steps, hipMemcpyDeviceToHost, s));
+  RC(spin_read(m));
   VSIM_HIP(hipStreamSynchronize(s));
   RC(spin_check(m));
   if (m->profile) RC(prof_collect(m));
@@ -1721,6 +1826,7 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
   if (N <= 0 || n_past < 0 || n_past + N > m->n_ctx) { set_error("eval: n_past + N exceeds n_ctx"); return VSIM_EINVAL; }
   m->st_npast = -1;  // an eval sets the device n_past: a stage step needs a new stage_begin
   VSIM_HIP(hipSetDevice(m->device));
+  const ErrScope es(m);
   RC(ensure_scratch(m, N));
   const int E = m->hp.n_embd, V = m->hp.n_vocab;
   hipStream_t s = m->stream;
@@ -1785,6 +1891,7 @@ int vsim_model_eval(vsim_model *m, int n_past, const int32_t *tokens, int N, con
       VSIM_HIP(hipMemcpyAsync(resid_out, m->inpL, sizeof(float) * N * E, hipMemcpyDeviceToDevice, s));
     }
   }
+  RC(spin_read(m));
   VSIM_HIP(hipStreamSynchronize(s));
   RC(spin_check(m));
   if (m->last && logits) memcpy(logits, m->logit_host, sizeof(float) * V);
@@ -1834,6 +1941,7 @@ int vsim_model_stage_step(vsim_model *m) {
   if (!m || m->st_npast < 0) { set_error("stage_step: stage_begin first"); return VSIM_EINVAL; }
   if (m->st_npast + 1 > m->n_ctx) { set_error("stage_step: context full"); return VSIM_EINVAL; }
   VSIM_HIP(hipSetDevice(m->device));
+  const ErrScope es(m);
   m->prof_npast = m->st_npast;
   if (m->graph_enabled && !m->profile) {
     RC(decode_graph(m, 3));
@@ -1846,6 +1954,7 @@ int vsim_model_stage_step(vsim_model *m) {
   }
   m->st_npast++;
   if (m->profile) {
+    RC(spin_read(m));
     VSIM_HIP(hipStreamSynchronize(m->stream));
     RC(spin_check(m));
     RC(prof_collect(m));
@@ -1884,6 +1993,7 @@ int vsim_model_debug_poison(vsim_model *m, int n_tokens) {
 int vsim_model_sync(vsim_model *m) {
   if (!m) { set_error("sync: null model"); return VSIM_EINVAL; }
   VSIM_HIP(hipSetDevice(m->device));
+  RC(spin_read(m));
   VSIM_HIP(hipStreamSynchronize(m->stream));
   return spin_check(m);
 }
