@@ -465,6 +465,38 @@ def pipeline_companion(args, world, rank, local, steps=64, warmup=8, limit=300):
             "scaling": d["scaling"], "steps": d["steps"], "config": d["config"]}
 
 
+def prefill_companion(limit=300):
+    """BASELINE.json configs[4] (codegen-16B, a 2048-token prompt on the fp16 MFMA dequant-GEMM
+    path) on the driver's clock: run_prefill in a child process with `limit` seconds, three timed
+    prompts after the first and one exact-mode prompt, so that a failure or a hang there cannot
+    take the headline decode measurement with it.  Reports ms per prompt, TFLOP/s and the
+    fraction of the dense fp16 MFMA peak, the first prompt, and the exact path's time."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK") and
+           not k.startswith("TORCHELASTIC_")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", "codegen-16B", "--prefill", "2048", "--steps", "3",
+           "--prefill-exact"]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=limit)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {limit} s"}
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not js:
+        return {"error": "no JSON line", "stdout_tail": r.stdout[-400:]}
+    d = json.loads(js[-1])
+    ex = d.get("exact_mode") or {}
+    return {"workload": d["config"]["workload"], "value": d["value"], "unit": d["unit"],
+            "ms_per_prompt": d["ms_per_prompt"], "first_prompt_ms": d["first_prompt_ms"], "steps": d["steps"],
+            "tflops": d["roofline"]["achieved"], "frac_of_dense_fp16_peak": d["roofline"]["frac"],
+            "exact_mode_ms_per_prompt": ex.get("ms_per_prompt"),
+            "parity": "fast prompt: per-op bound vs the reference's mul_mat, end to end cos >= 0.97 "
+                      "(tests/test_gpu_prefill.py); exact prompt: bit-identical to the oracle",
+            "wall_s": round(time.perf_counter() - t0, 1)}
+
+
 def run_prefill(args, dev):
     """One prompt eval of args.prefill tokens (codegen-16B, N = 2048) in
     fast mode: every Q4_0 matmul on fp16 MFMA after in-LDS dequant (gemm_f16.hip: for N >= 256
@@ -555,6 +587,8 @@ def main():
                     help="skip the GPT-NeoXT-20B layer-split companion measurement")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the bounded pythia-12b exact-decode companion measurement")
+    ap.add_argument("--no-prefill-companion", action="store_true",
+                    help="skip the bounded codegen-16B 2048-token prefill companion measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -671,6 +705,8 @@ def main():
     model.close()
     if rank == 0 and world == 1 and not args.no_other_configs and args.config == "gpt-j-6B" and args.mode == "exact":
         line["other_configs"] = {"pythia-12b": decode_companion("pythia-12b", dev)}
+    if rank == 0 and world == 1 and not args.no_prefill_companion and args.config == "gpt-j-6B" and args.mode == "exact":
+        line["prefill_codegen16b"] = prefill_companion()
     if not args.no_pipeline_20b and args.config == "gpt-j-6B":
         if dist is not None:
             dist.barrier()

@@ -13,7 +13,7 @@ fatal() { local rc=$1; echo "[gpu_round] $2 exit=$rc"; if [ "$rc" -ne 0 ]; then 
 # FETCH_SIZE passes first, installed as this round's profiles/<tag>_pmc_fetch_*.csv on this box,
 # so the bench line below reports traffic measured on the same commit in the same call
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_exact_$tag" -o run --output-format csv -- \
-  python3 "$root/bench.py" --steps 8 --warmup 2 --no-cpu-baseline --no-pipeline-20b --no-profile --no-fast --no-other-configs > "$out/pmc_exact_$tag.log" 2>&1
+  python3 "$root/bench.py" --steps 8 --warmup 2 --no-cpu-baseline --no-pipeline-20b --no-profile --no-fast --no-other-configs --no-prefill-companion > "$out/pmc_exact_$tag.log" 2>&1
 fatal $? pmc_exact
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fast_$tag" -o run --output-format csv -- \
   python3 "$root/bench.py" --mode fast --steps 8 --warmup 2 --no-cpu-baseline --no-pipeline-20b --no-profile > "$out/pmc_fast_$tag.log" 2>&1
@@ -29,7 +29,7 @@ fatal $? prefill; tail -1 "$out/bench_prefill_$tag.log"
 timeout -k 10 300 python3 "$root/bench.py" --config bloom-560m --steps 128 --no-cpu-baseline > "$out/bench_bloom_$tag.log" 2>&1
 fatal $? bloom; tail -1 "$out/bench_bloom_$tag.log" | cut -c1-200
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_exact_$tag" -o run --output-format csv -- \
-  python3 "$root/bench.py" --steps 64 --warmup 4 --no-cpu-baseline --no-pipeline-20b --no-fast --no-profile --no-other-configs > "$out/prof_exact_$tag.log" 2>&1
+  python3 "$root/bench.py" --steps 64 --warmup 4 --no-cpu-baseline --no-pipeline-20b --no-fast --no-profile --no-other-configs --no-prefill-companion > "$out/prof_exact_$tag.log" 2>&1
 fatal $? prof_exact
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof_fast_$tag" -o run --output-format csv -- \
   python3 "$root/bench.py" --mode fast --steps 64 --warmup 4 --no-cpu-baseline --no-pipeline-20b --no-profile > "$out/prof_fast_$tag.log" 2>&1

@@ -4,7 +4,8 @@ decode on the VSIM_NB_STAMPS build (tools/build_variant.sh nbstamps Makefile
 last tail of the run: per fc_out tile (the LN owner) the chain's end, the out-projection's
 granules seen, the partial sums published, every tile's partials seen, the block quantized;
 per out-projection tile the time its granules were stored.  Usage: VSIM_LIB=...nbstamps.so
-python tools/lnt_stamps.py [STEPS]"""
+python tools/lnt_stamps.py [STEPS [CONFIG]]  (CONFIG: gpt-j-6B, pythia-12b, gpt-neoxt-20b; 4 layers of
+the wider two, so the run stays short)"""
 import ctypes
 import os
 import sys
@@ -17,9 +18,12 @@ from vsim_amd import hip  # noqa: E402
 from vsim_amd import modelgen as mg  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-arch_s, hp = mg.CONFIGS["gpt-j-6B"]
-m = hip.Model.create(hip.ARCH_GPTJ, dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head, n_layer=hp.n_layer,
-                                         n_rot=hp.n_rot, use_parallel_residual=hp.use_parallel_residual),
+cfg = sys.argv[2] if len(sys.argv) > 2 else "gpt-j-6B"
+arch_s, hp = mg.CONFIGS[cfg]
+ARCH = {"gptj": hip.ARCH_GPTJ, "gptneox": hip.ARCH_GPTNEOX}
+m = hip.Model.create(ARCH[arch_s], dict(n_vocab=hp.n_vocab, n_embd=hp.n_embd, n_head=hp.n_head,
+                                        n_layer=hp.n_layer if cfg == "gpt-j-6B" else 4,
+                                        n_rot=hp.n_rot, use_parallel_residual=hp.use_parallel_residual),
                      n_ctx=512, device=0)
 m.randomize(seed=1234, std=0.02)
 m.set_mode(hip.MODE_EXACT)
@@ -32,7 +36,9 @@ f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert f(buf.ctypes.data, buf.nbytes) == 0
 m.close()
 
-nf, na, no = 128, 32, 128
+d = hp.n_embd // hp.n_head
+nsplit = 2 if d % 2 == 0 and (d // 2) % 32 == 0 else 1  # (model.cpp ATT_SPLIT)
+nf, na, no = hp.n_embd // 32, hp.n_head * nsplit, hp.n_embd // 32
 tl = buf[1536:1536 + nf + na + no, :16].astype(np.int64)
 t0 = tl[:, 0].min()
 us = lambda v: (v - t0) / 100.0  # noqa: E731
@@ -44,7 +50,7 @@ def q(name, v):
     print(f"  {name:34s} min {v.min():6.2f}  med {np.median(v):6.2f}  max {v.max():6.2f} us")
 
 
-print(f"last tail of a {steps}-step GPT-J-6B decode (position {5 + steps}), us from the first workgroup's start")
+print(f"last tail of a {steps}-step {cfg} decode (position {5 + steps}), us from the first workgroup's start")
 print("out-projection tiles:")
 q("start", op[:, 0])
 q("granules stored", op[:, 8])
@@ -60,3 +66,8 @@ last = int(np.argmax(fo[:, 8]))
 print(f"the last chain (tile {last}): entry {us(fo[last, 8]):.2f}, granules {us(fo[last, 9]):.2f}, "
       f"published {us(fo[last, 10]):.2f}, seen by all {us(fo[:, 11]).max():.2f} (first to see {us(fo[:, 11]).min():.2f}), "
       f"last block {us(fo[:, 12]).max():.2f}")
+ends = us(fo[:, 8])
+print("fc_out chain end by XCD (tile % 8), median / max:",
+      " ".join(f"{x}:{np.median(ends[x::8]):.2f}/{ends[x::8].max():.2f}" for x in range(8)))
+order = np.argsort(-ends)
+print("slowest fc_out tiles (index: chain end):", " ".join(f"{i}:{ends[i]:.2f}" for i in order[:10]))

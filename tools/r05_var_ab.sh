@@ -16,7 +16,7 @@ for rep in 1 2; do
     lib=""; ev="VSIM_NONE=0"
     case $v in product) ;; *=*) ev=$v ;; *) lib=$root/vsim_amd/_build/var/$v.so ;; esac
     env VSIM_LIB=$lib "$ev" timeout -k 10 200 python3 "$root/bench.py" --no-cpu-baseline --no-pipeline-20b --no-fast \
-      --no-other-configs ${BENCH_ARGS:-} > "$out/r05_${tag}_bench_${v}_${rep}.log" 2>&1
+      --no-other-configs --no-prefill-companion ${BENCH_ARGS:-} > "$out/r05_${tag}_bench_${v}_${rep}.log" 2>&1
     rc=$?; [ "$rc" -ne 0 ] && { echo "[bench $v] exit=$rc"; tail -5 "$out/r05_${tag}_bench_${v}_${rep}.log"; exit $rc; }
     python3 - "$out/r05_${tag}_bench_${v}_${rep}.log" "$v" <<'PY'
 import json, sys

@@ -415,23 +415,57 @@ __device__ __forceinline__ void lnt_oproj(const TailLn &N, int row, int rows, fl
   NBS(if (lane == 0) g_nb_stamps[1536 + blockIdx.x][8] = __builtin_amdgcn_s_memrealtime();)
 }
 
+// What the owner loads before its chain ends (a chunk early, so the loads land behind the last
+// adds): the out-projection's granule of the lane's row, the join's operands (the residual, the
+// two biases) and the affine of the lane's norm (lanes 0-31 norm 1, 32-63 norm 2)
+struct LntPre {
+  unsigned long long g;
+  float x, ab, fb, w, b;
+};
+__device__ __forceinline__ LntPre lnt_prefetch(const TailLn &N, int t) {
+  const int lane = threadIdx.x & 63, i = t * T32 + (lane & 31);
+  const bool hi = lane >= 32, mine = !hi || N.w2 != nullptr;
+  LntPre p;
+  p.g = ld_granule(N.og + i);
+  p.x = N.x[i];
+  p.ab = N.ab ? N.ab[i] : 0.0f;
+  p.fb = N.fb ? N.fb[i] : 0.0f;
+  p.w = mine ? (hi ? N.w2 : N.w1)[i] : 0.0f;
+  p.b = mine ? (hi ? N.b2 : N.b1)[i] : 0.0f;
+  return p;
+}
+// a double summed over each half-wave (lanes 0-31, 32-63), the sum in every lane of the half
+__device__ __forceinline__ double half_sum_d(double v) {
+  v = v + dpp::mov<dpp::QP_XOR1, 0xF>(v, 0.0);
+  v = v + dpp::mov<dpp::QP_XOR2, 0xF>(v, 0.0);
+  v = v + dpp::mov<dpp::HALF_MIRROR, 0xF>(v, 0.0);
+  v = v + dpp::mov<dpp::MIRROR, 0xF>(v, 0.0);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)(b & 0xFFFFFFFF), 0x401F), hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
+  return v + __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ int half_min_i(int v) {
+  v = min(v, dpp::mov<dpp::QP_XOR1, 0xF>(v, 0x7FFFFFFF));
+  v = min(v, dpp::mov<dpp::QP_XOR2, 0xF>(v, 0x7FFFFFFF));
+  v = min(v, dpp::mov<dpp::HALF_MIRROR, 0xF>(v, 0x7FFFFFFF));
+  v = min(v, dpp::mov<dpp::MIRROR, 0xF>(v, 0x7FFFFFFF));
+  return min(v, __builtin_amdgcn_ds_swizzle(v, 0x401F));
+}
+
 // fc_out tile t, wave 0: acc = row t*32 + (lane & 31) of fc_out (lanes 32-63 hold copies); pre:
-// the out-projection's granule of that row as loaded a chunk before the chain ended; scr: LDS
-// for E floats (the fallback's copy of the joined row)
-__device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, float acc, unsigned long long pre,
+// lnt_prefetch's loads, issued a chunk before the chain ended; scr: LDS for E floats (the
+// fallback's copy of the joined row)
+__device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, float acc, const LntPre &pre,
                                           float *scr, unsigned *err) {
   const int lane = threadIdx.x & 63, i = t * T32 + (lane & 31), n = ntile * T32;
   const unsigned tag = lnt_tag(N);
   NBS(unsigned long long *ls = g_nb_stamps[1536 + blockIdx.x] + 8;
       if (lane == 0) ls[0] = __builtin_amdgcn_s_memrealtime();)
-  // the join's and the affine's operands (earlier launches' data), loaded before any wait
   const bool hi = lane >= 32, two = N.w2 != nullptr, mine = !hi || two;
-  const float xv = N.x[i], abv = N.ab ? N.ab[i] : 0.0f, fbv = N.fb ? N.fb[i] : 0.0f;
-  const float *wp = hi ? N.w2 : N.w1, *bp = hi ? N.b2 : N.b1;
-  const float wv = mine ? wp[i] : 0.0f, bv = mine ? bp[i] : 0.0f;
+  const float xv = pre.x, abv = pre.ab, fbv = pre.fb, wv = pre.w, bv = pre.b;
   unsigned spins = 0;
   // 1. the out-projection's value of row i
-  unsigned long long ga = pre;
+  unsigned long long ga = pre.g;
   while (!__all((unsigned)(ga >> 32) == tag) && spins < LNT_SPIN_MAX) {
     lnt_spin(spins, err, lane);
     ga = ld_granule(N.og + i);
@@ -441,18 +475,11 @@ __device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, flo
   const float a = N.ab ? __uint_as_float((unsigned)ga) + abv : __uint_as_float((unsigned)ga);
   const float ff = N.fb ? acc + fbv : acc;
   const float v = xv + (a + ff);
-  if (lane < 32) {
-    N.jout[i] = v;
-    st_granule(N.jg + i, v, tag);
-  }
   {
-    double s = lane < 32 ? (double)v : 0.0, sa = lane < 32 ? (double)fabsf(v) : 0.0;
-    double q = lane < 32 ? (double)v * (double)v : 0.0;  // exact: 48-bit products
-    int um = lane < 32 ? ulp_exp(v) : (1 << 30);
-    s = wave_sum_d(s);
-    sa = wave_sum_d(sa);
-    q = wave_sum_d(q);
-    um = wave_min_i(um);
+    // (every lane holds a row of the tile: the half-wave sums are the tile's)
+    const double s = half_sum_d((double)v), sa = half_sum_d((double)fabsf(v));
+    const double q = half_sum_d((double)v * (double)v);  // exact squares: 48-bit products
+    const int um = half_min_i(ulp_exp(v));
     if (lane == 0) {
       float au = (float)sa;  // rounded up: an upper bound of sum |v| is all the certificate needs
       if ((double)au < sa) au = __uint_as_float(__float_as_uint(au) + 1u);
@@ -460,6 +487,10 @@ __device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, flo
       st16_sc1(N.rec + 2 * t, u32x4{(unsigned)sb, (unsigned)(sb >> 32), (unsigned)um, tag});
       st16_sc1(N.rec + 2 * t + 1, u32x4{(unsigned)qb, (unsigned)(qb >> 32), __float_as_uint(au), tag});
     }
+  }
+  if (lane < 32) {  // the joined row: the next layer's residual, and the fallback's granules
+    N.jout[i] = v;
+    st_granule(N.jg + i, v, tag);
   }
   NBS(if (lane == 0) ls[2] = __builtin_amdgcn_s_memrealtime();)
   // 3. every tile's partials: granule g = lane + 64 k (even g: {sum, umin}, odd g: {sum v^2, sum |v|})
@@ -523,11 +554,18 @@ __device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, flo
     const double s2 = (Q - 2.0 * t1) + t3, M = Q + 2.0 * fabs(t1) + t3;
     // |s2 - exact| <= ~20 u M (Q's tree, the three rounded terms); the reference's sequential
     // s2 lies within (n + 5) u of the exact value (ggml.c:4287-4291): both inside B
-    const double B = ((2.0 * n + 64.0) * (s2 > 0.0 ? s2 : 0.0) + 64.0 * M) * 0x1.0p-53 * (1.0 + 0x1.0p-20);
-    const float sc_lo = (float)(1.0 / sqrt((s2 + B) / n + eps));
-    const float sc_hi = (float)(1.0 / sqrt((s2 - B > 0.0 ? s2 - B : 0.0) / n + eps));
-    if (sc_lo == sc_hi)
-      scale = sc_lo;
+    const double s2c = s2 > 0.0 ? s2 : 0.0;
+    const double B = ((2.0 * n + 64.0) * s2c + 64.0 * M) * 0x1.0p-53 * (1.0 + 0x1.0p-20);
+    // r(S2) = 1/sqrt(S2/n + eps) moves by at most r * B / (2 (S2 + n eps)) over [s2 - B, s2 + B]
+    // (to first order; B / s2 <= 2^-30 wherever this passes), and the reference's and this
+    // evaluation of the double expression each round a few times (<= 2^-50 relative): when r
+    // widened by twice the first and four times the second still rounds to one float, that float
+    // is the reference's scale.  (One sqrt and one division instead of one per end.)
+    const double r = 1.0 / sqrt(s2 / n + eps);
+    const double dr = r * (B / (s2c + n * eps) + 0x1.0p-48);
+    const float sc = (float)r;
+    if ((float)(r - dr) == sc && (float)(r + dr) == sc)
+      scale = sc;
     else
       fallback = true;
   }
@@ -755,12 +793,12 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   rd(b0, 0, 0);
   rd(b1, 0, 1);
   rd(b2, 0, 2);
-  // (LNR 1: the out-projection's granule of this lane's row, loaded a chunk before the chain ends)
-  unsigned long long pre = 0;
+  // (LNR 1: the LayerNorm epilogue's operands, loaded a chunk before the chain ends)
+  LntPre pre{};
   const int c_pre = nch > 1 ? nch - 2 : 0;
   for (int c = 0; c < nch; ++c) {
     if constexpr (LNR == 1)
-      if (c == c_pre) pre = ld_granule(N->og + t * T32 + (lane & 31));
+      if (c == c_pre) pre = lnt_prefetch(*N, t);
     // the next chunk's count is read after batch NBQ-6's adds (behind the reads of batch NBQ-3,
     // so it lands with them) and compared at batch NBQ-3, before that chunk's first read; r05: read
     // at the chunk's top instead, it was often short by the chunk's last producers, and the
@@ -1046,12 +1084,19 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
       }
     };
     int ps = 0;
+    // (VSIM_NB_STAMPS: per producer wave, shader cycles summed over its steps: waiting for the
+    // factors and LDS stores (lgkmcnt(0)), computing, at the barrier -- rows 512 + workgroup,
+    // columns 12 + 3 pi ..; s_getreg of the 20-bit SHADER_CYCLES counter: no lgkmcnt)
+    NBS(unsigned st_fw = 0, st_comp = 0, st_bar = 0;
+        auto cyc = []() { return (unsigned)__builtin_amdgcn_s_getreg((29) | (0 << 6) | ((20 - 1) << 11)); };)
     auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
       ld(k + PF, qn, dqn);
+      NBS(const unsigned c0 = cyc();)
       // this chunk's factors (loaded a whole step ago) before the next chunk's loads go out:
       // scalar loads return out of order, so any later wait for them would be lgkmcnt(0)
       // and would also wait for the loads just issued
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      NBS(const unsigned c1 = cyc(); st_fw += (c1 - c0) & 0xFFFFF;)
       __builtin_amdgcn_sched_barrier(0);
       ldx(k + 1, xn);
       __builtin_amdgcn_sched_barrier(0);
@@ -1072,7 +1117,9 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
       }
       ps = ps == C5_RING - 1 ? 0 : ps + 1;
       __builtin_amdgcn_sched_barrier(0);
+      NBS(const unsigned c2 = cyc(); st_comp += (c2 - c1) & 0xFFFFF;)
       producer_barrier();
+      NBS(st_bar += (cyc() - c2) & 0xFFFFF;)
     };
     u32x4 q[PF + 1];
     float e[PF + 1];
@@ -1090,12 +1137,20 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
         step(k + u + 1, xb, xa, q[u + 1], e[u + 1], q[u % (PF + 1)], e[u % (PF + 1)]);
       }
     }
+    NBS(if (lane == 0 && gridDim.x < 512 && pi < 6) {
+      unsigned long long *st = g_nb_stamps[512 + blockIdx.x] + 12 + 3 * pi;
+      st[0] = st_fw;
+      st[1] = st_comp;
+      st[2] = st_bar;
+    })
     return;
   }
 
   // --------------------------------------------------------------- consumer
   float acc = 0.0f;
   float4 win[S::WIN];
+  NBS(unsigned sc_bar = 0;
+      auto ccyc = []() { return (unsigned)__builtin_amdgcn_s_getreg((29) | (0 << 6) | ((20 - 1) << 11)); };)
   const int crow = 64 * wave / 4 + lane;  // this consumer's row within the group
   auto src = [&](int c) { return &P[c % C5_RING][crow * S::LD]; };
   __builtin_amdgcn_s_setprio(3);
@@ -1128,8 +1183,14 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
         __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS read x6
       }
     }
+    NBS(const unsigned b0 = ccyc();)
     __syncthreads();
+    NBS(const unsigned b1 = ccyc(); sc_bar += (b1 - b0) & 0xFFFFF;)
   }
+  NBS(if (lane == 0 && wave == 0 && gridDim.x < 512) {
+    g_nb_stamps[512 + blockIdx.x][30] = sc_bar;
+    g_nb_stamps[512 + blockIdx.x][31] = nit;
+  })
   NBS(if (lane == 0 && wave == 0 && gridDim.x < 512) {
     unsigned long long *st = g_nb_stamps[512 + blockIdx.x];
     st[8] = c_m0;
