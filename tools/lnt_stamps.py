@@ -42,7 +42,7 @@ nf, na, no = hp.n_embd // 32, hp.n_head * nsplit, hp.n_embd // 32
 tl = buf[1536:1536 + nf + na + no, :16].astype(np.int64)
 t0 = tl[:, 0].min()
 us = lambda v: (v - t0) / 100.0  # noqa: E731
-fo, op = tl[:nf], tl[nf + na:]
+fo = tl[:nf]
 
 
 def q(name, v):
@@ -51,9 +51,13 @@ def q(name, v):
 
 
 print(f"last tail of a {steps}-step {cfg} decode (position {5 + steps}), us from the first workgroup's start")
-print("out-projection tiles:")
-q("start", op[:, 0])
-q("granules stored", op[:, 8])
+wk = tl[nf + na:]
+print(f"out-projection tiles ({len(wk)}):")
+q("start", wk[:, 0])
+q("granules stored", wk[:, 8])
+hd = tl[nf:nf + na]
+print(f"heads ({na} workgroups):")
+q("flag stored (end)", hd[:, 2])
 print("fc_out tiles (LN owners):")
 q("start", fo[:, 0])
 q("chain end (LN entry)", fo[:, 8])

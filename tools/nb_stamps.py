@@ -44,12 +44,13 @@ def role(name, rows, nprod, off):
 
 
 role("tail fc_out tiles", np.arange(0, 128), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
-role("tail out-proj tiles", np.arange(144 + (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0), 272 + (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0)), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
+NA = 32  # heads x 2 workgroups (r05 ATT_SPLIT)
+role("tail out-proj tiles", np.arange(128 + NA, 256 + NA), 8, [("dma wait", 4), ("slot wait", 12), ("compute", 20)])
 
 # the last tail's timeline (s_memrealtime, 100 MHz; rows 1536 + workgroup): fc_out tiles, QKV
 # workgroups (three consumers' ends), heads (count reached, end), out-projection (count, end)
 nf, nq = 128, (128 if os.environ.get("VSIM_TAIL_QKV", "0") == "1" else 0)
-na, no = 16, 128
+na, no = NA, 128
 tl = buf[1536:1536 + nf + nq + na + no, :8].astype(np.int64)
 t0 = tl[:, 0].min()
 us = lambda v: (v - t0) / 100.0  # noqa: E731

@@ -2,7 +2,8 @@
 diagnostic): GPT-J-6B exact decode on the VSIM_NB_STAMPS build, then per producer wave the shader
 cycles summed over its steps -- waiting at the step's lgkmcnt(0) (the scalar-loaded activation
 factors, and the previous step's LDS stores), computing the pair terms (and issuing their LDS
-stores), waiting at the chunk barrier -- and the consumer's cycles at its barriers, per chunk step;
+stores), waiting at the chunk barrier (s_memtime, summed over the steps) -- and the consumer's
+cycles at its barriers, per chunk step;
 split by whether the group's CU holds one group or two (HW_ID stamps of the same build).
 Usage: VSIM_LIB=vsim_amd/_build/var/nbstamps.so python tools/solo_stamps.py [STEPS]"""
 import ctypes

@@ -91,9 +91,7 @@ struct LnQuantJob {
   // row = x + ((ja + jab) + (jf + jfb)), stored to jout when non-null
   const float *ja, *jab, *jf, *jfb;
   float *jout;
-  unsigned *clear;  // non-null: clear[256 * l] zeroed for l < nclear (the layer tails' head counters)
-  int nclear;
-  unsigned *ep;     // non-null: the decode step's epoch, advanced by one (the tail LayerNorm's tags)
+  unsigned *ep;  // non-null: the decode step's epoch, advanced by one (the layer tails' tags, TailSync / TailLn)
 };
 
 // The next LayerNorm inside the layer tail (r06, k_layer_tail with TailJob::ln): the join
@@ -373,9 +371,18 @@ int attn_prefill_ldt(int nk);  // V^T row length (keys padded to the key tile)
 _Float16 *attn_prefill_k16(void *scratch, int E, int nk);
 _Float16 *attn_prefill_vt16(void *scratch, int E, int nk);
 size_t attn_prefill_scratch(int E, int nk);
+// The heads' completion flags of the layer tail (r06): one 8-byte {unused, tag} sc1 granule per head
+// workgroup, tag = epoch << 8 | layer + 1 (the epoch advanced by the step's first k_ln_quant), so
+// no counter has to be zeroed between layers or steps
+struct TailSync {
+  unsigned long long *hflag;  // [TAIL_MAX_HEADS]
+  const unsigned *ep;
+  int il;
+};
+constexpr int TAIL_MAX_HEADS = 128;
 // ln non-null (f and o one job each, both E rows): the tail also joins the residual and runs the
 // next LayerNorm(s) (TailLn); neither job's y is written (the joined row goes to ln->jout)
-int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
+int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, const TailSync &sy, int n_ctx,
                       hipStream_t s, const TailLn *ln = nullptr);
 // true when the tail LayerNorm can run for a model of width E on the current device (every
 // out-projection tile resident at once: E/32 tiles, one workgroup per CU)

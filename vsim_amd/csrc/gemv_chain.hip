@@ -556,13 +556,14 @@ __device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, flo
     // s2 lies within (n + 5) u of the exact value (ggml.c:4287-4291): both inside B
     const double s2c = s2 > 0.0 ? s2 : 0.0;
     const double B = ((2.0 * n + 64.0) * s2c + 64.0 * M) * 0x1.0p-53 * (1.0 + 0x1.0p-20);
-    // r(S2) = 1/sqrt(S2/n + eps) moves by at most r * B / (2 (S2 + n eps)) over [s2 - B, s2 + B]
-    // (to first order; B / s2 <= 2^-30 wherever this passes), and the reference's and this
-    // evaluation of the double expression each round a few times (<= 2^-50 relative): when r
-    // widened by twice the first and four times the second still rounds to one float, that float
-    // is the reference's scale.  (One sqrt and one division instead of one per end.)
+    // r(S2) = 1/sqrt(S2/n + eps) is decreasing and convex, so over [s2 - B, s2 + B] it moves by at
+    // most B |r'(s2 - B)| <= r * B / (2 (s2 - B + n eps)) * sqrt(1 + d), d = B / (s2 - B + n eps);
+    // for d <= 1 that is below r * B / (s2 - B + n eps), and for d > 1 the widening below exceeds r
+    // and the check fails.  The reference's and this evaluation of the double expression each round
+    // a few times (<= 2^-50 relative, four times covered): when r widened by both still rounds to
+    // one float, that float is the reference's scale.  (One sqrt and one division, not one per end.)
     const double r = 1.0 / sqrt(s2 / n + eps);
-    const double dr = r * (B / (s2c + n * eps) + 0x1.0p-48);
+    const double dr = r * (B / ((s2c - B > 0.0 ? s2c - B : 0.0) + n * eps) + 0x1.0p-48);
     const float sc = (float)r;
     if ((float)(r - dr) == sc && (float)(r + dr) == sc)
       scale = sc;
@@ -866,7 +867,9 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
 //   [nf, nf + na)    attention heads (attn.hpp; each head over nsplit workgroups, KQV columns
 //                    split); each stores the out-projection's operand write-through (sc1,
 //                    CO = true), drains it (vmcnt) and counts itself in *done (agent scope)
-//   [nf + na, ...)   out-projection tiles; wait until *done == na; their factor loads are sc1
+//   [nf + na, ...)   out-projection tiles; wait until every head's flag carries this step's tag
+//                    (r06: an 8-byte sc1 granule per head instead of one agent counter, which the
+//                    tiles saw ~3 us after the last head's add, profiles/r06_nb_stamps.txt); their factor loads are sc1
 //                    (device-coherent: they read past stale lines in the XCD's L2), so neither
 //                    side needs a fence.  r04: the release fence (an L2 write-back per head)
 //                    and the acquire (an L2 invalidate, which also dropped fc_out's lines)
@@ -874,16 +877,16 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
 //                    (profiles/r04_tail_headpath_ab.txt)
 // Waiting workgroups only wait for lower-indexed ones, which the dispatcher places first on
 // this part (and fc_out's tiles never wait, so the CUs they hold always come free); the wait
-// is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it the per-device error counter
-// is bumped, the tile goes on, and the executor fails the call (VSIM_ESPIN).  *done is zeroed by
-// the layer's LayerNorm kernel.  r05 A/B of the barrier-free hand-off against r04's per-chunk
+// is bounded all the same (TAIL_SPIN_MAX sleeps, ~1 s): past it the error counter is bumped, the
+// tile goes on, and the executor fails the call (VSIM_ESPIN).  r05 A/B of the barrier-free hand-off against r04's per-chunk
 // barrier (chain32_body): 31.4 vs 33.7 us per tail (profiles/r05_tail_nb_ab.txt); the barrier
 // tail is no longer built.
 constexpr unsigned TAIL_SPIN_MAX = 1u << 22;
 struct TailJob {
   GemvBatch f, o;
   AttnJob a;
-  unsigned *done, *err;
+  TailSync sy;  // the heads' flags
+  unsigned *err;
   int nf;
   int lnon;  // the next LayerNorm in this launch (TailLn)
   TailLn ln;
@@ -912,22 +915,28 @@ __global__ void __launch_bounds__(C2Tail::THREADS, 1) k_layer_tail(TailJob T) {
   }
   b -= T.nf;
   const int na = T.a.H * (T.a.nsplit > 1 ? T.a.nsplit : 1);
+  const unsigned htag = (*T.sy.ep << 8) | (unsigned)(T.sy.il + 1);
   if (b < na) {
     attn_body<C2Tail::THREADS, true>(T.a, b, L.a);
     NBS(if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through output stores landed
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(T.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) st_granule(T.sy.hflag + b, 0.0f, htag);  // (r06: was one agent counter)
     NBS(if (threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();)
     return;
   }
   b -= na;
-  if (threadIdx.x == 0) {
+  // wave 0 polls every head's flag (one or two per lane), the other waves wait at the barrier
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
     unsigned spins = 0;
-    while (__hip_atomic_load(T.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)na) {
-      __builtin_amdgcn_s_sleep(8);
+    for (;;) {
+      const bool ok = (lane >= na || (unsigned)(ld_granule(T.sy.hflag + lane) >> 32) == htag) &&
+                      (lane + 64 >= na || (unsigned)(ld_granule(T.sy.hflag + lane + 64) >> 32) == htag);
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(2);
       if (++spins == TAIL_SPIN_MAX) {
-        if (T.err) __hip_atomic_fetch_add(T.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (T.err && lane == 0) __hip_atomic_fetch_add(T.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -950,7 +959,7 @@ bool tail_ln_ok(int E) {
   return E % T32 == 0 && E / T32 <= LNT_MAX_TILES && E / T32 < cus;
 }
 
-int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, unsigned *done, int n_ctx,
+int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, const TailSync &sy, int n_ctx,
                       hipStream_t s, const TailLn *ln) {
   const int S = a.nsplit > 1 ? a.nsplit : 1;
   if (a.d % 32 != 0 || a.d > 256 || a.n_ctx != n_ctx || a.d % S != 0 || (a.d / S) % QK != 0 ||
@@ -966,7 +975,11 @@ int launch_layer_tail(const GemvBatch &f, const GemvBatch &o, const AttnJob &a, 
   T.f = f;
   T.o = o;
   T.a = a;
-  T.done = done;
+  T.sy = sy;
+  if (!sy.hflag || !sy.ep || sy.il < 0 || sy.il > 254 || a.H * S > TAIL_MAX_HEADS) {
+    set_error("layer tail: the heads' flags need a flag buffer, the step epoch, a layer below 255, at most 128 heads");
+    return VSIM_EINVAL;
+  }
   T.err = spin_error_counter();
   T.nf = 0;
   if (ln) {
@@ -1087,16 +1100,19 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
     // (VSIM_NB_STAMPS: per producer wave, shader cycles summed over its steps: waiting for the
     // factors and LDS stores (lgkmcnt(0)), computing, at the barrier -- rows 512 + workgroup,
     // columns 12 + 3 pi ..; s_getreg of the 20-bit SHADER_CYCLES counter: no lgkmcnt)
-    NBS(unsigned st_fw = 0, st_comp = 0, st_bar = 0;
-        auto cyc = []() { return (unsigned)__builtin_amdgcn_s_getreg((29) | (0 << 6) | ((20 - 1) << 11)); };)
+    NBS(unsigned long long st_fw = 0, st_comp = 0, st_bar = 0, pa = 0, pb = 0, pc = 0, pd = 0;
+        auto cyc = []() { return __builtin_amdgcn_s_memtime(); };)
     auto step = [&](int k, const f32x2 *xc, f32x2 *xn, const u32x4 &qc, float dqc, u32x4 &qn, float &dqn) {
       ld(k + PF, qn, dqn);
-      NBS(const unsigned c0 = cyc();)
+      // (stamps: s_memtime is a scalar-memory read; the previous step's four stamps are summed
+      // after this step's lgkmcnt(0), which they ride along, so no extra wait is added)
+      NBS(const unsigned long long c0 = cyc();)
       // this chunk's factors (loaded a whole step ago) before the next chunk's loads go out:
       // scalar loads return out of order, so any later wait for them would be lgkmcnt(0)
       // and would also wait for the loads just issued
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      NBS(const unsigned c1 = cyc(); st_fw += (c1 - c0) & 0xFFFFF;)
+      NBS(if (pa) { st_fw += pb - pa; st_comp += pc - pb; st_bar += pd - pc; }
+          pa = c0; pb = cyc();)
       __builtin_amdgcn_sched_barrier(0);
       ldx(k + 1, xn);
       __builtin_amdgcn_sched_barrier(0);
@@ -1117,9 +1133,9 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
       }
       ps = ps == C5_RING - 1 ? 0 : ps + 1;
       __builtin_amdgcn_sched_barrier(0);
-      NBS(const unsigned c2 = cyc(); st_comp += (c2 - c1) & 0xFFFFF;)
+      NBS(pc = cyc();)
       producer_barrier();
-      NBS(st_bar += (cyc() - c2) & 0xFFFFF;)
+      NBS(pd = cyc();)
     };
     u32x4 q[PF + 1];
     float e[PF + 1];
@@ -1149,8 +1165,8 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
   // --------------------------------------------------------------- consumer
   float acc = 0.0f;
   float4 win[S::WIN];
-  NBS(unsigned sc_bar = 0;
-      auto ccyc = []() { return (unsigned)__builtin_amdgcn_s_getreg((29) | (0 << 6) | ((20 - 1) << 11)); };)
+  NBS(unsigned long long sc_bar = 0;
+      auto ccyc = []() { return __builtin_amdgcn_s_memtime(); };)
   const int crow = 64 * wave / 4 + lane;  // this consumer's row within the group
   auto src = [&](int c) { return &P[c % C5_RING][crow * S::LD]; };
   __builtin_amdgcn_s_setprio(3);
@@ -1183,9 +1199,9 @@ __device__ __forceinline__ void solo_body(const GemvBatch &B, int g, float (*P)[
         __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS read x6
       }
     }
-    NBS(const unsigned b0 = ccyc();)
+    NBS(const unsigned long long b0 = ccyc();)
     __syncthreads();
-    NBS(const unsigned b1 = ccyc(); sc_bar += (b1 - b0) & 0xFFFFF;)
+    NBS(sc_bar += ccyc() - b0;)
   }
   NBS(if (lane == 0 && wave == 0 && gridDim.x < 512) {
     g_nb_stamps[512 + blockIdx.x][30] = sc_bar;

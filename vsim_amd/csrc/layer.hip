@@ -36,11 +36,7 @@ __global__ void __launch_bounds__(LNQ_THREADS) k_ln_quant(LnQuantJob j0, LnQuant
   extern __shared__ __attribute__((aligned(16))) float row[];
   const int part = blockIdx.x % LNQ_SPLIT;
   const LnQuantJob &J = blockIdx.x < LNQ_SPLIT ? j0 : j1;
-  if (blockIdx.x == 0) {
-    if (J.clear)
-      for (int l = threadIdx.x; l < J.nclear; l += LNQ_THREADS) J.clear[256 * l] = 0u;
-    if (J.ep && threadIdx.x == 0) *J.ep += 1u;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && J.ep) *J.ep += 1u;
   const int nb = n / QK;
   const int b0 = part * nb / LNQ_SPLIT, b1 = (part + 1) * nb / LNQ_SPLIT;  // this slice's blocks
   ln_quant_job<LNQ_THREADS>(J, row, n, part == 0 ? stats : nullptr, b0, b1);

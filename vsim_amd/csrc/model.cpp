@@ -110,12 +110,13 @@ struct vsim_model {
   hipGraphExec_t gexec_st = nullptr;
   int graph_st_mode = -1;
   int st_npast = -1;
-  unsigned *tail_done = nullptr;  // attention heads finished in the fused layer tail, one set per layer
+  unsigned *tail_done = nullptr;  // the fast decode step's per-head counters (fast_decode.hip)
   // the tail LayerNorm's hand-off buffers (TailLn): the step epoch, the out-projection's and the joined row's
   // granules [E], the per-tile partial sums [2 E/32]; zeroed at allocation (tag 0 never matches)
   unsigned *lnt_ep = nullptr;
   unsigned long long *lnt_og = nullptr, *lnt_jg = nullptr;
   uint4 *lnt_rec = nullptr;
+  unsigned long long *tail_hflag = nullptr;  // the tail heads' flags (TailSync), in the same allocation
   // fast-mode decode step (fast_decode.hip): fc_out split-K partial rows and attention
   // chunk partials (both consumed by the layer's k_fast_oproj_join)
   float *fast_ffp = nullptr, *fast_part = nullptr;
@@ -185,6 +186,7 @@ void free_scratch(vsim_model *m) {
   m->lnt_ep = nullptr;
   m->lnt_og = m->lnt_jg = nullptr;
   m->lnt_rec = nullptr;
+  m->tail_hflag = nullptr;
   if (m->pf_scratch) (void)hipFree(m->pf_scratch);
   m->pf_scratch = nullptr;
   if (m->pf_x16) (void)hipFree(m->pf_x16);
@@ -270,8 +272,9 @@ int ensure_scratch(vsim_model *m, int N) {
   VSIM_HIP(hipMalloc((void **)&m->tail_done, ncnt * sizeof(unsigned)));
   VSIM_HIP(hipMemset(m->tail_done, 0, ncnt * sizeof(unsigned)));
   {
-    // one allocation: epoch (own 256-byte line), og [E], jg [E], rec [2 E/32]
-    const size_t lb = 256 + 2 * E * sizeof(unsigned long long) + 2 * (E / QK) * sizeof(uint4);
+    // one allocation: epoch (own 256-byte line), og [E], jg [E], rec [2 E/32], the heads' flags
+    const size_t lb = 256 + 2 * E * sizeof(unsigned long long) + 2 * (E / QK) * sizeof(uint4) +
+                      TAIL_MAX_HEADS * sizeof(unsigned long long);
     uint8_t *p = nullptr;
     VSIM_HIP(hipMalloc((void **)&p, lb));
     VSIM_HIP(hipMemset(p, 0, lb));
@@ -279,6 +282,7 @@ int ensure_scratch(vsim_model *m, int N) {
     m->lnt_og = (unsigned long long *)(p + 256);
     m->lnt_jg = m->lnt_og + E;
     m->lnt_rec = (uint4 *)(m->lnt_jg + E);
+    m->tail_hflag = (unsigned long long *)(m->lnt_rec + 2 * (E / QK));
   }
   {
     const size_t d = E / H, nch = (m->n_ctx + FD_CHUNK - 1) / FD_CHUNK;
@@ -1032,10 +1036,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       // 1. (join +) input LayerNorm + quantize
       LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
       if (pending) join_into(j1, true);
-      if (tail) {
-        j1.clear = m->tail_done;
-        j1.nclear = 1;
-      }
+      if (tail && il == m->l0) j1.ep = m->lnt_ep;  // the step's epoch (the tail's flags)
       long ev = prof_begin(m);
       RC(launch_ln_quant(j1, nullptr, E, s));
       prof_end(m, ev, "k_ln_quant", ln_bytes(1, pending));
@@ -1056,7 +1057,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       if (tail) {
         GemvBatch none{};
         ev = prof_begin(m);
-        RC(launch_layer_tail(none, Bo, A, m->tail_done, m->n_ctx, s));
+        RC(launch_layer_tail(none, Bo, A, TailSync{m->tail_hflag, m->lnt_ep, il}, m->n_ctx, s));
         prof_end(m, ev, "k_layer_tail (attention + out-proj)", w4_algo_bytes(Bo.j[0].w) + kv_bytes);
         ++nk;
       } else {
@@ -1097,7 +1098,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       continue;
     }
     // 1. (join +) LayerNorm(s) + quantize, unless the previous layer's tail ran them (TailLn)
-    unsigned *done = m->tail_done + 256 * (il - m->l0);  // this layer's head counter
+    const TailSync sy{m->tail_hflag, m->lnt_ep, il};  // the heads' flags of this layer's tail
     long ev = -1;
     if (!ln_done) {
       LnQuantJob j1{R[cur], L.ln1_w, L.ln1_b, q1, d1, m->xd1};
@@ -1106,14 +1107,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
         join_into(j1, true);
         join_into(j2, false);
       }
-      if (tail && il == m->l0) {  // the step's first norm: every layer's counter, the epoch
-        j1.clear = m->tail_done;
-        j1.nclear = m->l1 - m->l0;
-        j1.ep = m->lnt_ep;
-      } else if (tail) {
-        j1.clear = done;
-        j1.nclear = 1;
-      }
+      if (tail && il == m->l0) j1.ep = m->lnt_ep;  // the step's first norm advances the epoch
       ev = prof_begin(m);
       RC(launch_ln_quant(j1, gptj ? nullptr : &j2, E, s));
       prof_end(m, ev, "k_ln_quant", ln_bytes(gptj ? 1 : 2, pending));
@@ -1178,7 +1172,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
       N.stats = dev_stats();
       N.il = il;
       ev = prof_begin(m);
-      RC(launch_layer_tail(Bf, Bo, A, done, m->n_ctx, s, &N));
+      RC(launch_layer_tail(Bf, Bo, A, sy, m->n_ctx, s, &N));
       prof_end(m, ev, "k_layer_tail (fc_out + attention + out-proj + join + LayerNorm)",
                w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + kv_bytes + ln_bytes(N.w2 ? 2 : 1, true));
       ++nk;
@@ -1189,7 +1183,7 @@ int enqueue_decode(vsim_model *m, int &nk) {
     }
     if (tail) {
       ev = prof_begin(m);
-      RC(launch_layer_tail(Bf, Bo, A, done, m->n_ctx, s));
+      RC(launch_layer_tail(Bf, Bo, A, sy, m->n_ctx, s));
       prof_end(m, ev, "k_layer_tail (fc_out + attention + out-proj)",
                w4_algo_bytes(Bf.j[0].w) + w4_algo_bytes(Bo.j[0].w) + kv_bytes);
       ++nk;
