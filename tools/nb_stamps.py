@@ -63,7 +63,7 @@ def tlrow(name, rows, cols):
 
 
 print("tail timeline (us from the first workgroup's start):")
-tlrow("fc_out", np.arange(0, nf), [("dma issued", 4), ("chunk 0 landed", 5), ("chunk 1 landed", 6), ("chunk 0 computed", 7), ("chunk 0 ready", 3), ("end", 2)])
+tlrow("fc_out", np.arange(0, nf), [("dma issued", 4), ("chunk 0 landed", 5), ("chunk 0 counted", 7), ("consumer has chunk 0", 3), ("end", 2)])
 if nq:
     tlrow("QKV", np.arange(nf, nf + nq), [("Q end", 1), ("K end", 2), ("V end", 3)])
 tlrow("heads", np.arange(nf + nq, nf + nq + na), [("attn", 1), ("end", 2)])
@@ -87,3 +87,21 @@ for i in list(order[:8]) + list(order[60:64]):
     print(f"  {i:4d} {i % 8} {us(fo[i, 2]):6.2f} {b[2] / nchk:7.0f} {np.median(b[12:20]) / nchk:7.0f} {np.median(b[4:12]) / nchk:7.0f}"
           f" {cyc:9.0f} {dur:6.2f} {cyc / dur / 1e3:5.2f}")
 print("end-time quartiles:", np.percentile(us(fo[:, 2]), [0, 25, 50, 75, 100]).round(2))
+
+# per chunk of the last tail's fc_out tiles (rows 960/1088/1216 + tile: the consumer's wait for
+# chunk c, the time it asked for chunk c (its wait_ready: three batches before chunk c-1 ends), the
+# time chunk c's last producer counted itself)
+cw = buf[960:1088].astype(np.int64)
+cs = buf[1088:1216].astype(np.int64)
+if cs[:, 1].any():
+    nchk = int(np.median(buf[:128, 3]))
+    print("fc_out per chunk (medians over the tiles, shader cycles): c, consumer wait, asked(c) - asked(c-1)")
+    for c in range(min(nchk, 32)):
+        ln = np.median(cs[:, c] - cs[:, c - 1]) if c > 0 else float("nan")
+        print(f"  {c:3d} {np.median(cw[:, c]):7.0f} {ln:7.0f}")
+    print("fc_out producers (p, wave: dma wait, slot wait, compute per chunk; medians over tiles)")
+    for p, w in enumerate([1, 2, 3, 5, 6, 7, 9, 10]):
+        print(f"  p{p} w{w:2d}: {np.median(buf[:128, 4 + p] / nchk):6.0f} {np.median(buf[:128, 12 + p] / nchk):6.0f}"
+              f" {np.median(buf[:128, 20 + p] / nchk):6.0f}")
+if os.environ.get("NB_STAMPS_SAVE"):
+    np.save(os.environ["NB_STAMPS_SAVE"], buf)

@@ -653,10 +653,16 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   const int nb = J.w.k / QK, nch = (nb + CB - 1) / CB;
   if (threadIdx.x < NB_RING) L.ready[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.cons = 0;
+#if defined(VSIM_ABL_NOWAIT) || defined(VSIM_ABL_NOPROD)  // (ablations: finite terms in an unwritten ring)
+  for (int i = threadIdx.x; i < NB_RING * 32 * LD; i += blockDim.x) (&L.P[0][0])[i] = 0.0f;
+#endif
   __syncthreads();
   if (S::FILL && wave > 0 && wave % 4 == 0) return;  // the consumer's SIMD is left to it
 
   if (wave > 0) {
+#ifdef VSIM_ABL_NOPROD  // timing-only ablation: no producers (wrong results)
+    if (S::FILL) return;
+#endif
     // ------------------------------------------------------------- producer
     const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
     if (p >= NPW) return;  // (a launch wider than this shape needs)
@@ -723,14 +729,18 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       NBS(sw_comp += __builtin_amdgcn_s_memtime() - t1;)
       if (lane == 0) __hip_atomic_fetch_add(&L.ready[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // (stamps: fc_out tiles' startup, producer 0: chunk 0 counted)
+      NBS(if (ONE && LNR == 1 && p == 0 && k == 0 && lane == 0) g_nb_stamps[1536 + blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();)
       dma(k + 1 + DEPTH);
     };
 #pragma unroll
     for (int c = 0; c < DEPTH; ++c) dma(c);
+    NBS(if (ONE && LNR == 1 && p == 0 && lane == 0) g_nb_stamps[1536 + blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();)
     uint4 qa, qb;
     float da, db, fa0, fa1, fb0, fb1;
     issue_raw(0, qa, da, fa0, fa1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    NBS(if (ONE && LNR == 1 && p == 0 && lane == 0) g_nb_stamps[1536 + blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();)
     dma(DEPTH);
     for (int k = 0; k < nch; k += 2) {
       issue_raw(k + 1, qb, db, fb0, fb1);
@@ -762,6 +772,9 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   // (the re-poll is asm: a C++ loop of LDS loads made the compiler drain every read in flight
   // where its path joins the fast one, once per chunk)
   auto wait_ready = [&](int c, unsigned have) {
+#ifdef VSIM_ABL_NOWAIT  // timing-only ablation: the consumer never waits (wrong results)
+    return;
+#endif
     NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
     if (have < need(c)) {
       unsigned spins = 0, h;
@@ -780,11 +793,16 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
           : "vcc", "scc", "memory");
       if (spins >= NB_SPIN_MAX && err && lane == 0) __hip_atomic_fetch_add(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    NBS(cw += __builtin_amdgcn_s_memtime() - t0;)
+    NBS(const unsigned long long dw = __builtin_amdgcn_s_memtime() - t0; cw += dw;
+        if (ONE && blockIdx.x < 128 && c < 32 && lane == 0) {
+          g_nb_stamps[960 + blockIdx.x][c] = dw;
+          g_nb_stamps[1088 + blockIdx.x][c] = t0;
+        })
   };
   __builtin_amdgcn_s_setprio(3);
   NBS(const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();)
   wait_ready(0, 0u);
+  NBS(if (ONE && LNR == 1 && lane == 0) g_nb_stamps[1536 + blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();)
   f32x4 b0[BQ], b1[BQ], b2[BQ], b3[BQ];
   auto rd = [&](f32x4 (&d)[BQ], int c, int q) {  // batch q of chunk c (past the last chunk: harmless)
     const f32x4 *src = (const f32x4 *)&L.P[c % NB_RING][lr * LD] + 2 * q * BQ + lk;

@@ -1,10 +1,11 @@
 // vsim_amd/csrc/layer.hip — fused kernels of the single-token decode step.
 //
 // One decoder layer (vsim.cpp:521-696 for GPT-NeoX with parallel residual, the same ops for
-// GPT-J) = 3 launches in exact mode:
+// GPT-J) = 2 launches in exact mode since r06 (3 for layer 0 and the serial fallback):
 //   1. k_ln_quant      (the previous layer's residual join +) LayerNorm(s) + affine +
 //                      activation quantization (ggml.c:4246, 5024-5041): inpL -> Q4_0
-//                      activation row(s) and their xd factors
+//                      activation row(s) and their xd factors; layer 0 only when the tail
+//                      runs the next LayerNorm itself (gemv_chain.hip, TailLn)
 //   2. GEMV batch      {fc_in, Q, K, V} in one launch; fc_in's epilogue adds the bias, looks
 //                      up GELU and quantizes each 32-row tile into the fc_out activation
 //   3. k_layer_tail    (gemv_chain.hip) fc_out beside the attention heads (attn.hpp: RoPE,
