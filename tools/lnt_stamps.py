@@ -40,6 +40,7 @@ d = hp.n_embd // hp.n_head
 nsplit = 2 if d % 2 == 0 and (d // 2) % 32 == 0 else 1  # (model.cpp ATT_SPLIT)
 nf, na, no = hp.n_embd // 32, hp.n_head * nsplit, hp.n_embd // 32
 tl = buf[1536:1536 + nf + na + no, :16].astype(np.int64)
+spn = buf[1536:1536 + nf, 13:15].astype(np.int64)  # the owners' re-polls: granule, partials
 t0 = tl[:, 0].min()
 us = lambda v: (v - t0) / 100.0  # noqa: E731
 fo = tl[:nf]
@@ -75,3 +76,5 @@ print("fc_out chain end by XCD (tile % 8), median / max:",
       " ".join(f"{x}:{np.median(ends[x::8]):.2f}/{ends[x::8].max():.2f}" for x in range(8)))
 order = np.argsort(-ends)
 print("slowest fc_out tiles (index: chain end):", " ".join(f"{i}:{ends[i]:.2f}" for i in order[:10]))
+print("owners' re-polls (count: tiles) -- granule:", dict(zip(*np.unique(spn[:, 0], return_counts=True))),
+      " partials: median", int(np.median(spn[:, 1])), "max", int(spn[:, 1].max()))

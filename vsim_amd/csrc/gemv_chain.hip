@@ -470,7 +470,10 @@ __device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, flo
     lnt_spin(spins, err, lane);
     ga = ld_granule(N.og + i);
   }
-  NBS(if (lane == 0) ls[1] = __builtin_amdgcn_s_memrealtime();)
+  NBS(if (lane == 0) {
+    ls[1] = __builtin_amdgcn_s_memrealtime();
+    ls[5] = spins;  // (the granule's re-polls)
+  })
   // 2. the join (ja + jab) + (jf + jfb), then x + that (kern.hpp ln_exact_lds_t's join)
   const float a = N.ab ? __uint_as_float((unsigned)ga) + abv : __uint_as_float((unsigned)ga);
   const float ff = N.fb ? acc + fbv : acc;
@@ -537,7 +540,10 @@ __device__ __forceinline__ void lnt_owner(const TailLn &N, int t, int ntile, flo
     }
     lnt_spin(spins, err, lane);
   }
-  NBS(if (lane == 0) ls[3] = __builtin_amdgcn_s_memrealtime();)
+  NBS(if (lane == 0) {
+    ls[3] = __builtin_amdgcn_s_memrealtime();
+    ls[6] = spins;  // (the partials' re-polls)
+  })
   S = wave_sum_d(S);
   Q = wave_sum_d(Q);
   A = wave_sum_d(A);
