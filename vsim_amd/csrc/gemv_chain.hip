@@ -659,16 +659,10 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   const int nb = J.w.k / QK, nch = (nb + CB - 1) / CB;
   if (threadIdx.x < NB_RING) L.ready[threadIdx.x] = 0;
   if (threadIdx.x == 0) L.cons = 0;
-#if defined(VSIM_ABL_NOWAIT) || defined(VSIM_ABL_NOPROD)  // (ablations: finite terms in an unwritten ring)
-  for (int i = threadIdx.x; i < NB_RING * 32 * LD; i += blockDim.x) (&L.P[0][0])[i] = 0.0f;
-#endif
   __syncthreads();
   if (S::FILL && wave > 0 && wave % 4 == 0) return;  // the consumer's SIMD is left to it
 
   if (wave > 0) {
-#ifdef VSIM_ABL_NOPROD  // timing-only ablation: no producers (wrong results)
-    if (S::FILL) return;
-#endif
     // ------------------------------------------------------------- producer
     const int p = S::FILL ? wave - 1 - wave / 4 : wave - 1, r = lane & 31, hb = lane >> 5;
     if (p >= NPW) return;  // (a launch wider than this shape needs)
@@ -778,9 +772,6 @@ __device__ __forceinline__ void chain32_nb_body(const GemvBatch &B, int t, NbLds
   // (the re-poll is asm: a C++ loop of LDS loads made the compiler drain every read in flight
   // where its path joins the fast one, once per chunk)
   auto wait_ready = [&](int c, unsigned have) {
-#ifdef VSIM_ABL_NOWAIT  // timing-only ablation: the consumer never waits (wrong results)
-    return;
-#endif
     NBS(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
     if (have < need(c)) {
       unsigned spins = 0, h;
