@@ -109,7 +109,7 @@ int vsim_graph_profile_report(char *buf, size_t cap);
 /* Decode fast path of vsim_graph_compute.  A single-token eval of gptneox_eval
  * (vsim.cpp:470-747, use_parallel_residual = 1) is recognised node by node (42 nodes per
  * layer in ggml_build_forward_expand order, plus get_rows and the final norm + lm_head) and
- * runs as the model executor's fused decode step -- 3 launches per layer, replayed as one
+ * runs as the model executor's fused decode step -- 2 launches per layer (since r06), replayed as one
  * hipGraph -- on the weights and KV cache the per-node path mirrored, with the KQV grouping of
  * cgraph->n_threads.  Every other graph (prompt batches, the serial residual) runs per node.
  * VSIM_GRAPH_FAST=0 turns the fast path off.

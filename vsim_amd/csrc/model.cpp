@@ -905,14 +905,16 @@ int enqueue_decode_fast(vsim_model *m, int &nk) {
   return VSIM_OK;
 }
 
-// Exact mode: the single-token decode step as 3 fused launches per layer (layer.hip,
+// Exact mode: the single-token decode step as fused launches per layer (layer.hip,
 // gemv_chain.hip).  Reads the token from tok_dev and n_past from npast_dev, so the enqueued
 // sequence is replayable (hipGraph).
 //   1. k_ln_quant: (join of the previous layer +) input LayerNorm (+ post_attention
-//      LayerNorm for GPT-NeoX), quantized
+//      LayerNorm for GPT-NeoX), quantized -- since r06 only for the first layer of the step
+//      (or when the previous tail could not run it, TailLn)
 //   2. k_gemv_solo: {fc_in (+ bias, GELU, requantize), Q, K, V}
-//   3. k_layer_tail: fc_out beside the attention heads and the out-projection; no biases
-//      (they join in the next layer's step 1)
+//   3. k_layer_tail: fc_out beside the attention heads and the out-projection, then the join
+//      and the next layer's LayerNorm(s) (or the final norm) quantized (TailLn; without it the
+//      biases join in the next step 1)
 // fc_out's K = 4E chain (vsim.cpp:680-690) is the layer's longest dependency, so the
 // attention branch fills the CUs beside it instead of running before it.
 // Serial-residual graphs (BLOOM; GPT-NeoX with use_parallel_residual = 0, vsim.cpp:626-658)
